@@ -1,0 +1,90 @@
+"""The CPU oracle reproduces the reference's recorded outputs (pins the oracle).
+
+Fixtures come from tests/golden/make_golden.py (reference run with recorded RNG draws).
+The oracle replays the same draws and must match bit for bit: same ATen op sequence on
+the same inputs.
+"""
+import pytest
+import torch
+
+from conftest import golden_names, load_golden
+from oracle import vbn_oracle as O
+from vectorizedbayesiannetwork_amd.model import model_from_checkpoint
+
+
+def _run_case(model, case):
+    q = case["query"]
+    n = case["n_samples"]
+    draws = O.ReplayDraws(case["draws"])
+    eng = case["engine"]
+    p = case["params"]
+    if eng == "monte_carlo_marginalization":
+        pdf, xs = O.monte_carlo_marginalization(model, q["target"], q["evidence"], q["do"], n, draws)
+        out = {"pdf": pdf, "samples": xs}
+    elif eng == "likelihood_weighting":
+        w, xs = O.likelihood_weighting(model, q["target"], q["evidence"], q["do"], n, draws,
+                                       normalize=p.get("normalize", True))
+        out = {"pdf": w, "samples": xs}
+    elif eng == "importance_sampling":
+        w, xs, ess, fb = O.importance_sampling(model, q["target"], q["evidence"], q["do"], n, draws,
+                                               ess_threshold=p.get("ess_threshold", 0.1))
+        out = {"pdf": w, "samples": xs, "ess": ess, "fallback": fb}
+    elif eng == "ancestral":
+        out = {"samples": O.ancestral(model, q["target"], q["evidence"], q["do"], n, draws)}
+    else:
+        raise AssertionError(eng)
+    assert draws.exhausted(), "oracle consumed fewer draws than the reference"
+    return out
+
+
+def _eq(a, b):
+    if isinstance(a, bool):
+        return a == b
+    return a.shape == b.shape and torch.equal(torch.nan_to_num(a, nan=123.0), torch.nan_to_num(b, nan=123.0)) \
+        and torch.equal(a.isnan(), b.isnan())
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_oracle_matches_reference_bitwise(name):
+    fx = load_golden(name)
+    model = model_from_checkpoint(fx["model"])
+    n_checked = 0
+    for case in fx["cases"]:
+        if case["engine"] == "cpd":
+            rec = model.cpds[case["node"]]
+            draws = O.ReplayDraws(case["draws"])
+            s = O.cpd_sample(rec, case["parents"], case["n_samples"], draws)
+            assert draws.exhausted()
+            assert _eq(s, case["outputs"]["sample"]), (name, case["node"])
+            lp = O.cpd_log_prob(rec, s, case["parents"])
+            assert _eq(lp, case["outputs"]["log_prob_sampled"]), (name, case["node"])
+            if "x" in case:
+                lpx = O.cpd_log_prob(rec, case["x"], case["parents"])
+                assert _eq(lpx, case["outputs"]["log_prob_x"]), (name, case["node"])
+            n_checked += 1
+            continue
+        out = _run_case(model, case)
+        for k, ref in case["outputs"].items():
+            assert _eq(out[k], ref), (name, case["engine"], case["params"], k)
+        n_checked += 1
+    assert n_checked == len(fx["cases"])
+
+
+def test_fixture_exercises_semantics():
+    """The fixture set covers the quirks parity must reproduce."""
+    seen = set()
+    for name in golden_names():
+        for case in load_golden(name)["cases"]:
+            out = case["outputs"]
+            if case["engine"] == "importance_sampling":
+                seen.add(("is_fallback", out["fallback"]))
+                if torch.isnan(out["pdf"]).any():
+                    seen.add("is_nan_rows")
+            if case["engine"] == "monte_carlo_marginalization":
+                q = case["query"]
+                if q["target"] in q["do"]:
+                    seen.add("mcm_do_target")
+                if out["pdf"].shape[0] == 1 and len(next(iter(q["evidence"].values()), torch.zeros(2, 1))) > 1:
+                    seen.add("mcm_root_target_1xS")
+    assert {("is_fallback", True), ("is_fallback", False), "is_nan_rows", "mcm_do_target",
+            "mcm_root_target_1xS"} <= seen, seen

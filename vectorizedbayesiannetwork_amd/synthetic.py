@@ -1,0 +1,83 @@
+"""Synthetic workloads of SURVEY.md §8(d): random DAG, linear-Gaussian SEM data, queries.
+
+These generators are shared by the golden-fixture script (which fits models with the
+reference), the tests and ``bench.py`` (which builds random-init models of the same
+architecture, see :mod:`vectorizedbayesiannetwork_amd.model`).
+
+* DAG: nodes ``x0..x{N-1}``; for i >= 1 draw ``k = rng.randint(0, min(3, i))`` parents
+  with ``rng.sample(range(i), k)`` (``rng = random.Random(seed)``), edges inserted in
+  that order (the order fixes the parent-concat order, reference ``core/dags.py:31-33``).
+* Data: ``x = 0.3 * N(0,1) + 0.5 * sum(parents)`` over ``nx.topological_sort`` with a
+  ``torch.Generator().manual_seed(seed)``.
+* Query: target = last node of the topological order; evidence =
+  ``random.Random(seed).sample(topo[:-1], N // 4)``.
+"""
+from __future__ import annotations
+
+import random
+from typing import Dict, List, Sequence, Tuple
+
+import networkx as nx
+import torch
+
+__all__ = [
+    "random_dag",
+    "sem_data",
+    "round_robin_kinds",
+    "default_query_nodes",
+    "CONFIGS",
+]
+
+
+def random_dag(n_nodes: int, seed: int = 0, max_parents: int = 3) -> nx.DiGraph:
+    rng = random.Random(seed)
+    g = nx.DiGraph()
+    names = [f"x{i}" for i in range(n_nodes)]
+    g.add_nodes_from(names)
+    for i in range(1, n_nodes):
+        k = rng.randint(0, min(max_parents, i))
+        for j in rng.sample(range(i), k):
+            g.add_edge(names[j], names[i])
+    return g
+
+
+def sem_data(g: nx.DiGraph, n_rows: int, seed: int = 0) -> Dict[str, torch.Tensor]:
+    gen = torch.Generator().manual_seed(seed)
+    out: Dict[str, torch.Tensor] = {}
+    for node in nx.topological_sort(g):
+        x = 0.3 * torch.randn(n_rows, generator=gen)
+        for p in g.predecessors(node):
+            x = x + 0.5 * out[p][:, 0]
+        out[node] = x.unsqueeze(-1)
+    return out
+
+
+def round_robin_kinds(g: nx.DiGraph, kinds: Sequence[str]) -> Dict[str, str]:
+    return {node: kinds[i % len(kinds)] for i, node in enumerate(g.nodes)}
+
+
+def default_query_nodes(g: nx.DiGraph, seed: int = 1) -> Tuple[str, List[str]]:
+    topo = list(nx.topological_sort(g))
+    target = topo[-1]
+    evidence = random.Random(seed).sample(topo[:-1], len(g.nodes) // 4)
+    return target, evidence
+
+
+# BASELINE.json "configs" (index 0..4). B = queries, S = samples per query.
+CONFIGS = {
+    "cfg1": dict(name="readme-3node-gaussian_nn-mcm", n_nodes=3, kinds=("gaussian_nn",),
+                 engine="monte_carlo_marginalization", B=1, S=200),
+    "cfg2": dict(name="32node-gaussian_nn-mcm", n_nodes=32, kinds=("gaussian_nn",),
+                 engine="monte_carlo_marginalization", B=4096, S=1024, rows=2048),
+    "cfg3": dict(name="32node-mdn+softmax_nn-is", n_nodes=32, kinds=("mdn", "softmax_nn"),
+                 engine="importance_sampling", B=4096, S=1024, rows=2048),
+    "cfg4": dict(name="64node-kde10k-mcm", n_nodes=64, kinds=("kde",),
+                 engine="monte_carlo_marginalization", B=4096, S=1024, rows=10000,
+                 kde_max_points=10000),
+    "cfg5": dict(name="128node-mixed-mcm", n_nodes=128,
+                 kinds=("gaussian_nn", "linear_gaussian", "mdn", "kde", "softmax_nn"),
+                 engine="monte_carlo_marginalization", B=65536, S=2048, rows=8192,
+                 kde_max_points=4096),
+    "anchor64": dict(name="64node-gaussian_nn-mcm", n_nodes=64, kinds=("gaussian_nn",),
+                     engine="monte_carlo_marginalization", B=4096, S=1024, rows=2048),
+}
