@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Throughput of ``VBN.infer_posterior`` on MI355X (BASELINE.json metric).
+
+A step = one ``infer_posterior`` call over one batch of synthetic queries:
+default workload cfg2 = 32-node random DAG, gaussian_nn CPDs (random-init weights of the
+reference architecture, data-derived standardisation), 4096 queries x 1024 samples per GPU,
+monte_carlo_marginalization.  With N GPUs every rank runs its own 4096-query shard (weak
+scaling, global query index feeds the RNG); there is no data-path collective.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|anchor64]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Rank 0 prints one JSON line.  ``roofline`` prices the dominant kernel (vbn_walk_kernel) with
+HIP events on the stream it runs on; ``cpu_baseline`` times the CPU oracle (the reference's
+torch op sequence, oracle/vbn_oracle.py) on a bounded sample on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from vectorizedbayesiannetwork_amd import VBN, synthetic  # noqa: E402
+from vectorizedbayesiannetwork_amd.engines import AncestralSampler, Query  # noqa: E402
+from vectorizedbayesiannetwork_amd.model import random_init_model  # noqa: E402
+from vectorizedbayesiannetwork_amd.plan import KIND_ID  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 (vector = f32 MFMA), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def build_workload(cfg_name: str, device: str, rank: int):
+    cfg = dict(synthetic.CONFIGS[cfg_name])
+    g = synthetic.random_dag(cfg["n_nodes"], seed=0)
+    data = synthetic.sem_data(g, cfg.get("rows", 2048), seed=0)
+    kinds = synthetic.round_robin_kinds(g, cfg["kinds"])
+    overrides = {"kde": {"max_points": cfg["kde_max_points"]}} if "kde_max_points" in cfg else None
+    model = random_init_model(g, kinds, data, seed=0, overrides=overrides)
+    vbn = VBN.from_model(model, device=device)
+    target, ev_nodes = synthetic.default_query_nodes(g, seed=1)
+    B, S = cfg["B"], cfg["S"]
+    # on-manifold evidence: B rows of the model's own ancestral draw (seed 2 + rank)
+    torch.manual_seed(2 + rank)
+    joint = AncestralSampler(n_samples=B).sample(vbn, Query(target=None, evidence={}, do={}), n_samples=B)
+    evidence = {n: joint[n][0].contiguous() for n in ev_nodes}
+    query = {"target": target, "evidence": evidence}
+    return cfg, g, model, vbn, query
+
+
+def mlp_flops_per_particle(model, plan) -> float:
+    """Algorithmic FLOPs of one particle in one walk: 2 x MACs of every MLP evaluated
+    (in->32->32->out) plus 2 x MACs of linear_gaussian means."""
+    fl = 0.0
+    for i in range(plan.n_steps):
+        row = plan.steps[i].tolist()
+        kind, role, flags, nin, n_out = row[0], row[1], row[2], row[4], row[10]
+        if role == 0 or (role == 2 and not (flags & 1)):
+            continue
+        if kind in (KIND_ID["gaussian_nn"], KIND_ID["mdn"], KIND_ID["softmax_nn"]) and not (flags & 2):
+            fl += 2.0 * (32 * nin + 32 * 32 + 32 * n_out)
+        elif kind == KIND_ID["linear_gaussian"]:
+            fl += 2.0 * nin * row[7]
+    return fl
+
+
+def kde_pairs_per_particle(model, plan) -> float:
+    pairs = 0.0
+    for i in range(plan.n_steps):
+        row = plan.steps[i].tolist()
+        if row[0] != KIND_ID["kde"] or row[1] == 0:
+            continue
+        m = row[9]
+        if row[1] == 1 and not (row[2] & 2):
+            pairs += m * (1 + 1.0 / 16)          # CDF pass + one chunk rescan
+        if row[2] & 1:
+            pairs += m                           # log_prob pass
+    return pairs
+
+
+def cpu_baseline(cfg, model, query, n_queries: int, reps: int = 3):
+    """Oracle (reference op sequence, TorchDraws = the reference's RNG calls) on host cores."""
+    from oracle import vbn_oracle as O
+    threads = torch.get_num_threads()
+    ev = {k: v[:n_queries].cpu() for k, v in query["evidence"].items()}
+    S = cfg["S"]
+    eng = cfg["engine"]
+
+    def one():
+        with torch.no_grad():
+            if eng == "monte_carlo_marginalization":
+                O.monte_carlo_marginalization(model, query["target"], ev, {}, S, O.TorchDraws())
+            else:
+                O.importance_sampling(model, query["target"], ev, {}, S, O.TorchDraws())
+
+    one()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        one()
+        ts.append(time.perf_counter() - t0)
+    med = statistics.median(ts)
+    return {"value": n_queries / med, "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{n_queries} queries x {S} samples, median of {reps} after 1 warm-up, "
+                      f"torch CPU {threads} threads, no_grad"}
+
+
+def load_traffic(cfg_name: str):
+    """Per-launch HBM bytes of vbn_walk_kernel from the committed PMC summary (profiles/)."""
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*{cfg_name}*pmc*.json")))
+    if not paths:
+        return None
+    try:
+        with open(paths[-1]) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-queries", type=int, default=0)
+    ap.add_argument("--prune-barren", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    device = f"cuda:{local}"
+
+    cfg, g, model, vbn, query = build_workload(args.config, device, rank)
+    B, S = cfg["B"], cfg["S"]
+    vbn.set_inference_method(cfg["engine"], n_samples=S, q_base=rank * B,
+                             prune_barren=args.prune_barren)
+    if cfg["engine"] == "importance_sampling":
+        vbn._inference._lw.q_base = rank * B
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+
+    for _ in range(args.warmup):
+        vbn.infer_posterior(query)
+    torch.cuda.synchronize()
+
+    # timed region: exactly K steps, barrier + synchronize on both sides
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pdf, samples = vbn.infer_posterior(query)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = world * B * args.steps / elapsed
+
+    # dominant kernel: walk launch duration with HIP events on its stream
+    from vectorizedbayesiannetwork_amd import engines as E
+    last = dict(E.LAST_LAUNCH)                # the walk the timed steps launched
+    pk, plan, fixed = last["pk"], last["plan"], last["fixed"]
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = max(3, min(args.steps, 10))
+    E.run_walk(pk, plan, fixed, B, S, seed=1)
+    ev0.record(stream)
+    for i in range(reps):
+        E.run_walk(pk, plan, fixed, B, S, seed=i + 2)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = ev0.elapsed_time(ev1) / reps
+    flops = mlp_flops_per_particle(model, plan) * B * S
+    pairs = kde_pairs_per_particle(model, plan) * B * S
+    traffic = load_traffic(args.config)
+    if pairs > 0.1 * flops / 64:
+        roof = {"bound": "valu-exp", "achieved": pairs / (kern_ms * 1e-3) / 1e12, "peak": None,
+                "unit": "Tpair/s", "frac": None, "traffic": traffic}
+    else:
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "kernel": "vbn_walk_kernel", "kernel_ms": round(kern_ms, 4),
+                "flops_per_launch": flops, "launches_timed": reps}
+
+    out = {
+        "metric": "posterior queries/sec (infer_posterior, n_samples=1024) at 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SURVEY §8d DAG/SEM/query generator; random-init CPD weights)",
+        "config": {"workload": f"{args.config}: {cfg['name']}", "queries_per_gpu": B, "global_batch": B * world,
+                   "n_samples": S, "n_nodes": cfg["n_nodes"], "engine": cfg["engine"],
+                   "parallelism": f"query-sharded dp{world}", "prune_barren": args.prune_barren},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        nq = args.cpu_queries or (1024 if cfg["engine"] == "monte_carlo_marginalization" and cfg["n_nodes"] <= 64
+                                  and "kde" not in cfg["kinds"] else 8)
+        out["cpu_baseline"] = cpu_baseline(cfg, model, query, nq)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,132 @@
+/*
+ * vbn_hip.h — C-ABI of the MI355X (gfx950) batched Bayesian-network inference path.
+ *
+ * Plain pointers and sizes only (no torch types).  All device pointers are HIP device
+ * memory; every call is asynchronous on the given hipStream_t (passed as void*).  Return
+ * value: 0 on success, otherwise a hipError_t / VBN_E_* code; vbn_hip_last_error() gives
+ * the message of the last failure on the calling thread.
+ *
+ * What each entry point replaces in the reference (Giovannibriglia/VectorizedBayesianNetwork):
+ *
+ *   vbn_hip_walk            the topological particle pass shared by
+ *                             MonteCarloMarginalization.infer_posterior
+ *                               (vbn/inference/monte_carlo_marginalization.py:18-92),
+ *                             ImportanceSampling.infer_posterior, sampling loop + log-weights
+ *                               (vbn/inference/importance_sampling.py:24-80),
+ *                             LikelihoodWeighting.infer_posterior
+ *                               (vbn/inference/likelihood_weighting.py:24-71),
+ *                             _ancestral_sample_tensor (vbn/sampling/ancestral.py:13-41),
+ *                           and, through single-step plans with per-particle fixed inputs,
+ *                           the per-node BaseCPD.sample / log_prob (vbn/core/base.py:45-59) of
+ *                             GaussianNNCPD   (vbn/cpds/gaussian_nn.py:215-288)
+ *                             LinearGaussianCPD (vbn/cpds/linear_gaussian.py:163-217)
+ *                             MDNCPD          (vbn/cpds/mdn.py:185-272)
+ *                             KDECPD          (vbn/cpds/kde.py:105-182)
+ *                             SoftmaxNNCPD    (vbn/cpds/softmax_nn.py:581-759).
+ *   vbn_hip_normalize_weights  torch.softmax(log_weights, 1) + ESS
+ *                               (importance_sampling.py:82-84) and the normalize / max-shift
+ *                               branch of likelihood_weighting.py:75-80.
+ */
+#ifndef VBN_HIP_H
+#define VBN_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VBN_ABI_VERSION 1
+
+/* error codes besides hipError_t values */
+#define VBN_E_ARGS 1001
+#define VBN_E_LDS 1002
+
+/* CPD kinds (reference registry keys) */
+enum vbn_kind {
+  VBN_KIND_GAUSSIAN_NN = 0,
+  VBN_KIND_LINEAR_GAUSSIAN = 1,
+  VBN_KIND_MDN = 2,
+  VBN_KIND_KDE = 3,
+  VBN_KIND_SOFTMAX_NN = 4
+};
+
+/* role of a node for one query signature */
+enum vbn_role { VBN_ROLE_SKIP = 0, VBN_ROLE_LATENT = 1, VBN_ROLE_FIXED = 2 };
+
+/* step flags */
+#define VBN_F_LOGP 1        /* add log p(value | parents) to the particle's accumulator */
+#define VBN_F_ROOT 2        /* CPD without parents                                        */
+#define VBN_F_SHARED 4      /* draws shared across queries (root nodes in MCM/LW/ancestral) */
+#define VBN_F_STANDARDIZE 8 /* MLP input (x-mean)/std (gaussian_nn)                          */
+#define VBN_F_CLIP 16       /* softmax_nn within_bin_clip                                      */
+
+/* activations of the NN CPDs (reference gaussian_nn.py:19-24) */
+enum vbn_act { VBN_ACT_RELU = 0, VBN_ACT_TANH = 1, VBN_ACT_GELU = 2, VBN_ACT_ELU = 3 };
+
+/* softmax_nn within-bin densities (softmax_nn.py:665-679) */
+enum vbn_within { VBN_WITHIN_UNIFORM = 0, VBN_WITHIN_TRIANGULAR = 1, VBN_WITHIN_GAUSSIAN = 2 };
+
+/* engine modes: what happens to the accumulated log-probability at the end */
+enum vbn_mode {
+  VBN_MODE_MCM = 0,       /* out_lp = exp(lp)          (pdf)          */
+  VBN_MODE_WEIGHTED = 1,  /* out_lp = lp               (log-weights)  */
+  VBN_MODE_SAMPLE = 2     /* no out_lp                                */
+};
+
+/* One node of the topological walk (32 x int32, filled by the host plan packer). */
+typedef struct vbn_step {
+  int32_t kind, role, flags, act;
+  int32_t n_in, in_off, out_col, out_dim;
+  int32_t fixed_col, k, n_out, node_id;
+  int32_t noise_idx, aux0, aux1, aux2;
+  int32_t off_std, off_w1, off_w2, off_b2, off_w3, off_b3, off_tail, off_pts;
+  int32_t reserved[8];
+} vbn_step;
+
+/* Arguments of one particle walk over B queries x S samples. */
+typedef struct vbn_walk_args {
+  const vbn_step* steps;   /* [n_steps] device                                   */
+  const int32_t* in_cols;  /* parent column slots, indexed by step.in_off          */
+  const float* params;     /* parameter blob                                       */
+  const float* fixed;      /* fixed values: [rows][fixed_ld], rows = B or B*S        */
+  const float* noise;      /* optional injected draws [n_noise][2][noise_b][S][dmax] */
+  const int32_t* out_cols; /* slots written to out_x per particle                   */
+  float* out_lp;           /* [B*S] or NULL                                        */
+  float* out_x;            /* [B*S][n_out_cols] or NULL                            */
+  int64_t n_queries;       /* B                                                    */
+  int32_t n_samples;       /* S                                                    */
+  int32_t n_steps;
+  int32_t n_slots;         /* LDS value slots per particle                          */
+  int32_t max_out;         /* widest MLP head (LDS scratch rows)                     */
+  int32_t fixed_ld;
+  int32_t fixed_per_particle;
+  int32_t noise_b;
+  int32_t dmax;
+  int32_t n_out_cols;
+  int32_t mode;            /* enum vbn_mode                                        */
+  int64_t q_base;          /* global index of query 0 (multi-GPU shards)            */
+  uint64_t seed;
+  uint64_t offset;         /* RNG stream offset (one per engine call)               */
+} vbn_walk_args;
+
+int vbn_hip_abi_version(void);
+const char* vbn_hip_last_error(void);
+
+/* Topological particle walk (see header comment). */
+int vbn_hip_walk(const vbn_walk_args* args, void* stream);
+
+/* Per-query weight normalisation over S particles.
+ *   normalize=1: w = softmax(log_w) per row, ess[b] = 1/sum(w^2)
+ *   normalize=0: w = max(exp(log_w - max(log_w)), eps), ess untouched (may be NULL).
+ * log_w and w may alias. */
+int vbn_hip_normalize_weights(const float* log_w, float* w, float* ess, int64_t n_queries,
+                              int32_t n_samples, int32_t normalize, float eps, void* stream);
+
+/* LDS bytes one 64-particle wave needs for a plan (host helper). */
+int64_t vbn_hip_lds_bytes(int32_t n_slots, int32_t max_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VBN_HIP_H */

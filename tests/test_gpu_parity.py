@@ -1,0 +1,143 @@
+"""HIP path vs the oracle on the golden fixtures (same recorded draws injected).
+
+Tolerances (fp32; the MLPs' sums are reassociated by MFMA/FMA vs the CPU sgemm):
+  samples / target values : |d| <= 1e-4 + 1e-4 |x|
+  pdf (MCM)               : |d| <= 1e-6 + 2e-3 |pdf|     (log-density abs error ~1e-4..1e-3)
+  IS/LW weights           : |d| <= 1e-6 + 2e-3 |w|
+  ESS                     : rel 2e-3
+  softmax_nn bin indices  : bit-exact (checked through the bin-boundary log_prob cases)
+  IS fallback decision    : identical
+All run through the C-ABI library (vbn_hip_walk / vbn_hip_normalize_weights).
+"""
+import math
+
+import pytest
+import torch
+
+from conftest import golden_names, load_golden
+from golden_noise import noise_dict
+from oracle import vbn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+S_ATOL, S_RTOL = 1e-4, 1e-4
+P_ATOL, P_RTOL = 1e-6, 2e-3
+
+
+def _vbn(fx):
+    from vectorizedbayesiannetwork_amd import VBN
+    from vectorizedbayesiannetwork_amd.model import model_from_checkpoint
+    model = model_from_checkpoint(fx["model"])
+    return model, VBN.from_model(model, device="cuda")
+
+
+def _close(name, got, ref, atol, rtol):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    assert got.shape == ref.shape, f"{name}: shape {tuple(got.shape)} vs {tuple(ref.shape)}"
+    nan_g, nan_r = torch.isnan(got), torch.isnan(ref)
+    assert torch.equal(nan_g, nan_r), f"{name}: NaN pattern differs"
+    inf_ok = torch.equal(torch.isinf(got) & (got > 0), torch.isinf(ref) & (ref > 0)) and \
+        torch.equal(torch.isinf(got) & (got < 0), torch.isinf(ref) & (ref < 0))
+    assert inf_ok, f"{name}: inf pattern differs"
+    m = ~(nan_g | torch.isinf(ref))
+    err = (got[m] - ref[m]).abs()
+    tol = atol + rtol * ref[m].abs()
+    bad = (err > tol)
+    assert not bad.any(), f"{name}: {int(bad.sum())} of {err.numel()} out of tolerance, max err {float(err.max()):.3g}"
+    return float(err.max()) if err.numel() else 0.0
+
+
+def _cases():
+    out = []
+    for name in golden_names():
+        for i, case in enumerate(load_golden(name)["cases"]):
+            out.append(pytest.param(name, i, id=f"{name}-{i}-{case['engine']}"))
+    return out
+
+
+@pytest.mark.parametrize("name,idx", _cases())
+def test_golden_case_on_gpu(name, idx):
+    from vectorizedbayesiannetwork_amd import cpd as C
+    from vectorizedbayesiannetwork_amd.engines import (AncestralSampler, ImportanceSampling,
+                                                       LikelihoodWeighting, MonteCarloMarginalization)
+    fx = load_golden(name)
+    case = fx["cases"][idx]
+    model, vbn = _vbn(fx)
+    eng = case["engine"]
+    n = case["n_samples"]
+    nd0 = noise_dict(case, model, 0)
+    if eng == "cpd":
+        node = case["node"]
+        rec = model.cpds[node]
+        par = case["parents"]
+        xs = C.cpd_sample(vbn, node, None if par is None else par.cuda(), n, _noise=nd0)
+        ref = O.cpd_sample(rec, par, n, O.ReplayDraws(case["draws"]))
+        _close("cpd.sample", xs, ref, S_ATOL, S_RTOL)
+        lp = C.cpd_log_prob(vbn, node, ref.cuda(), None if par is None else par.cuda())
+        _close("cpd.log_prob(sampled)", lp, O.cpd_log_prob(rec, ref, par), 2e-4, 1e-4)
+        if "x" in case:
+            lpx = C.cpd_log_prob(vbn, node, case["x"].cuda(), None if par is None else par.cuda())
+            _close("cpd.log_prob(x)", lpx, O.cpd_log_prob(rec, case["x"], par), 2e-4, 1e-4)
+        return
+    q = case["query"]
+    qq = vbn._normalize_query(q)
+    p = case["params"]
+    draws = O.ReplayDraws(case["draws"])
+    if eng == "monte_carlo_marginalization":
+        pdf, xs = MonteCarloMarginalization(n_samples=n).infer_posterior(vbn, qq, _noise=nd0)
+        rpdf, rxs = O.monte_carlo_marginalization(model, q["target"], q["evidence"], q["do"], n, draws)
+        _close("samples", xs, rxs, S_ATOL, S_RTOL)
+        _close("pdf", pdf, rpdf, P_ATOL, P_RTOL)
+    elif eng == "likelihood_weighting":
+        e = LikelihoodWeighting(n_samples=n, normalize=p.get("normalize", True))
+        w, xs = e.infer_posterior(vbn, qq, _noise=nd0)
+        rw, rxs = O.likelihood_weighting(model, q["target"], q["evidence"], q["do"], n, draws,
+                                         normalize=p.get("normalize", True))
+        _close("samples", xs, rxs, S_ATOL, S_RTOL)
+        _close("weights", w, rw, P_ATOL, P_RTOL)
+    elif eng == "importance_sampling":
+        e = ImportanceSampling(n_samples=n)
+        e.ess_threshold = p.get("ess_threshold", 0.1)
+        w, xs = e.infer_posterior(vbn, qq, _noise=nd0, _noise_fallback=noise_dict(case, model, 1))
+        rw, rxs, ress, rfb = O.importance_sampling(model, q["target"], q["evidence"], q["do"], n, draws,
+                                                   ess_threshold=e.ess_threshold)
+        assert e._last_fallback == rfb == case["outputs"]["fallback"]
+        _close("ess", e._last_ess, ress, 1e-5, P_RTOL)
+        _close("samples", xs, rxs, S_ATOL, S_RTOL)
+        _close("weights", w, rw, P_ATOL, P_RTOL)
+    elif eng == "ancestral":
+        xs = AncestralSampler(n_samples=n).sample(vbn, qq, n, _noise=nd0)
+        rxs = O.ancestral(model, q["target"], q["evidence"], q["do"], n, draws)
+        _close("samples", xs, rxs, S_ATOL, S_RTOL)
+    else:
+        raise AssertionError(eng)
+
+
+def test_softmax_bins_bit_exact_on_gpu():
+    """Values exactly on bin edges and outside the range land in the reference bins
+    (tests/test_cpds.py:66-82): log_prob picks log_softmax[bin] + within-bin density, so an
+    off-by-one bin shows as a different finite value or a different -inf pattern."""
+    from vectorizedbayesiannetwork_amd import cpd as C
+    seen = 0
+    for name in golden_names():
+        fx = load_golden(name)
+        model, vbn = _vbn(fx)
+        for node, rec in model.cpds.items():
+            if rec.kind != "softmax_nn" or bool(rec.state["_is_discrete"].any()):
+                continue
+            edges = rec.state["_bin_edges"]
+            xs = torch.cat([edges.t(), edges[:, :1].t() - 3.0, edges[:, -1:].t() + 3.0], 0)  # [C+3, D]
+            nb = xs.shape[0]
+            par = None
+            if model.parents[node]:
+                par = torch.zeros(nb, rec.input_dim)
+            got = C.cpd_log_prob(vbn, node, xs.cuda(), None if par is None else par.cuda()).cpu()
+            ref = O.cpd_log_prob(rec, xs, par)
+            assert torch.equal(torch.isinf(got), torch.isinf(ref)), (name, node)
+            fin = torch.isfinite(ref)
+            assert torch.allclose(got[fin], ref[fin], atol=2e-4, rtol=1e-4), (name, node)
+            bins = O.smx_x_to_bin(rec, xs.unsqueeze(1))
+            assert int(bins.min()) >= 0 and int(bins.max()) <= int(rec.hp("n_classes")) - 1
+            seen += 1
+    assert seen >= 3

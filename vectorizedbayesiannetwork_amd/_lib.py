@@ -1,0 +1,103 @@
+"""Loader for ``libvbn_hip.so`` (the C-ABI of include/vbn_hip.h) via ctypes.
+
+The library is built in-tree by ``__graft_entry__.build()`` / ``make -C
+vectorizedbayesiannetwork_amd/csrc``.  There is no CPU fallback: if the library is missing
+or cannot be loaded, every accelerated entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
+ABI_VERSION = 1
+
+# exported symbols declared in include/vbn_hip.h
+EXPORTS = (
+    "vbn_hip_abi_version",
+    "vbn_hip_last_error",
+    "vbn_hip_walk",
+    "vbn_hip_normalize_weights",
+    "vbn_hip_lds_bytes",
+)
+
+
+class VbnWalkArgs(ctypes.Structure):
+    """Mirror of ``vbn_walk_args`` (include/vbn_hip.h)."""
+
+    _fields_ = [
+        ("steps", ctypes.c_void_p),
+        ("in_cols", ctypes.c_void_p),
+        ("params", ctypes.c_void_p),
+        ("fixed", ctypes.c_void_p),
+        ("noise", ctypes.c_void_p),
+        ("out_cols", ctypes.c_void_p),
+        ("out_lp", ctypes.c_void_p),
+        ("out_x", ctypes.c_void_p),
+        ("n_queries", ctypes.c_int64),
+        ("n_samples", ctypes.c_int32),
+        ("n_steps", ctypes.c_int32),
+        ("n_slots", ctypes.c_int32),
+        ("max_out", ctypes.c_int32),
+        ("fixed_ld", ctypes.c_int32),
+        ("fixed_per_particle", ctypes.c_int32),
+        ("noise_b", ctypes.c_int32),
+        ("dmax", ctypes.c_int32),
+        ("n_out_cols", ctypes.c_int32),
+        ("mode", ctypes.c_int32),
+        ("q_base", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+        ("offset", ctypes.c_uint64),
+    ]
+
+
+class VbnHipError(RuntimeError):
+    pass
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path: str = None) -> ctypes.CDLL:
+    """Load and type the library (torch must be imported first so the HIP runtime that
+    torch bundles is the one the library binds to)."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise VbnHipError(
+                f"HIP library not found at {p}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` "
+                "(no CPU fallback exists for the accelerated path)")
+        import torch  # noqa: F401  (binds libamdhip64 first)
+        lib = ctypes.CDLL(p)
+        for name in EXPORTS:
+            if not hasattr(lib, name):
+                raise VbnHipError(f"{p} does not export {name}")
+        lib.vbn_hip_abi_version.restype = ctypes.c_int
+        lib.vbn_hip_last_error.restype = ctypes.c_char_p
+        lib.vbn_hip_walk.argtypes = [ctypes.POINTER(VbnWalkArgs), ctypes.c_void_p]
+        lib.vbn_hip_walk.restype = ctypes.c_int
+        lib.vbn_hip_normalize_weights.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+            ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
+        lib.vbn_hip_normalize_weights.restype = ctypes.c_int
+        lib.vbn_hip_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
+        lib.vbn_hip_lds_bytes.restype = ctypes.c_int64
+        v = lib.vbn_hip_abi_version()
+        if v != ABI_VERSION:
+            raise VbnHipError(f"{p}: ABI version {v}, expected {ABI_VERSION}")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().vbn_hip_last_error().decode(errors="replace")
+        raise VbnHipError(f"{what} failed ({rc}): {msg}")

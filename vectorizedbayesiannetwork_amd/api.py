@@ -1,0 +1,244 @@
+"""VBN-compatible facade over the accelerated path.
+
+Mirrors the reference's public surface for this path (reference ``vbn/vbn.py``):
+
+* ``VBN.set_inference_method(method, **kw)`` / ``set_sampling_method`` accept a registry
+  name, a ``{"name": ...}`` dict, a :class:`ConfigItem` (``vbn.config.inference.<name>``)
+  or a callable, and merge YAML defaults with keyword overrides (vbn.py:257-335);
+* ``VBN.infer_posterior(query, **kw) -> (pdf[B,S], samples[B,S,Dt])`` (vbn.py:474-481);
+* ``VBN.sample(query, n_samples, **kw)`` (vbn.py:570-577);
+* query normalisation and its errors (vbn.py:579-618).
+
+Models come from the reference checkpoint format (``VBN.load``), a live fitted reference
+object (``VBN.from_reference``) or an in-memory :class:`BNModel` (``VBN.from_model``).
+Training (``fit``/``update``) stays with the reference; this package consumes its output.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from types import SimpleNamespace
+from typing import Any, Dict, List, Optional
+
+import networkx as nx
+import torch
+
+from .engines import Query, infer_batch_size
+from .model import BNModel, load_checkpoint, model_from_checkpoint, model_from_vbn
+from .registry import INFERENCE_REGISTRY, SAMPLING_REGISTRY
+
+__all__ = ["VBN", "ConfigItem", "defaults"]
+
+
+# Packaged defaults of the in-scope engines (reference vbn/configs/inference/*.yaml,
+# vbn/configs/sampling/ancestral.yaml).
+_ENGINE_DEFAULTS = {
+    "inference": {
+        "monte_carlo_marginalization": {"n_samples": 1024},
+        "importance_sampling": {"n_samples": 1024},
+        "likelihood_weighting": {"n_samples": 1024, "eps": 1e-12, "normalize": True},
+    },
+    "sampling": {"ancestral": {"n_samples": 512}},
+}
+
+
+@dataclass
+class ConfigItem:
+    """reference vbn.py:37-51"""
+
+    name: str
+    params: Dict
+    kind: Optional[str] = None
+
+    def to_dict(self) -> Dict[str, Any]:
+        return {"name": self.name, **self.params}
+
+    def as_dict(self) -> Dict[str, Any]:
+        return self.to_dict()
+
+
+class ConfigNamespace(SimpleNamespace):
+    def __getitem__(self, item):
+        return getattr(self, item)
+
+
+def _load_configs() -> ConfigNamespace:
+    cats = {}
+    for cat, items in _ENGINE_DEFAULTS.items():
+        cats[cat] = ConfigNamespace(**{k: ConfigItem(name=k, params=dict(v), kind=cat) for k, v in items.items()})
+    return ConfigNamespace(**cats)
+
+
+class _Defaults:
+    def inference(self, name) -> Dict:
+        name = getattr(name, "name", name)
+        return {"name": name, **dict(_ENGINE_DEFAULTS["inference"][name])}
+
+    def sampling(self, name) -> Dict:
+        name = getattr(name, "name", name)
+        return {"name": name, **dict(_ENGINE_DEFAULTS["sampling"][name])}
+
+
+defaults = _Defaults()
+
+
+class _DAG:
+    """Topology view with the reference StaticDAG interface (core/dags.py:23-45)."""
+
+    def __init__(self, model: BNModel):
+        self._m = model
+
+    def nodes(self) -> List[str]:
+        return list(self._m.nodes)
+
+    def edges(self):
+        return list(self._m.edges)
+
+    def parents(self, node: str) -> List[str]:
+        return list(self._m.parents.get(node, []))
+
+    def topological_order(self) -> List[str]:
+        return list(self._m.topo)
+
+
+def _resolve(method, registry, kind: str, kwargs):
+    if isinstance(method, dict):
+        name = method.get("name") or method.get("method")
+        if name is None:
+            raise TypeError("method dict must include a 'name' field")
+        if not isinstance(name, str):
+            raise TypeError("method name must be a string")
+        key = name.lower().strip()
+        if key not in registry:
+            raise ValueError(f"Unknown {kind} method '{name}'. Available: {list(registry.keys())}")
+        base = {k: v for k, v in method.items() if k not in {"name", "method"}}
+        return key, {**base, **kwargs}
+    if isinstance(method, ConfigItem) or (hasattr(method, "name") and hasattr(method, "params")):
+        return method.name, {**dict(method.params), **kwargs}
+    if isinstance(method, str):
+        key = method.lower().strip()
+        if key not in registry:
+            raise ValueError(f"Unknown {kind} method '{method}'. Available: {list(registry.keys())}")
+        return key, dict(kwargs)
+    if callable(method):
+        return method, {}
+    raise TypeError("method must be a string, ConfigItem, or callable")
+
+
+class VBN:
+    """Accelerated VBN: same inference/sampling surface, GPU execution."""
+
+    def __init__(self, model: BNModel, seed: Optional[int] = None, device: Optional[str] = None):
+        if device is None or str(device) == "auto":
+            device = "cuda"
+        self.device = torch.device(device)
+        self.seed = seed
+        if seed is not None:
+            torch.manual_seed(seed)
+        self.model = model
+        self.dag = _DAG(model)
+        self.nodes = model.cpds
+        self.config = _load_configs()
+        self._inference = None
+        self._sampling = None
+        self._inference_config = None
+        self._sampling_config = None
+
+    # ---- construction -------------------------------------------------------------------
+    @classmethod
+    def from_model(cls, model: BNModel, device: Optional[str] = None, seed: Optional[int] = None) -> "VBN":
+        return cls(model, seed=seed, device=device)
+
+    @classmethod
+    def load(cls, path_or_ckpt, *, map_location: str = "cuda") -> "VBN":
+        """Load a reference ``VBN.save`` checkpoint (weights_only; reference vbn.py:736-824)."""
+        ckpt = load_checkpoint(path_or_ckpt) if isinstance(path_or_ckpt, str) else path_or_ckpt
+        model = model_from_checkpoint(ckpt)
+        seed = (ckpt.get("meta") or {}).get("seed")
+        vbn = cls(model, seed=seed, device=map_location)
+        cfg = ckpt.get("config") or {}
+        inf = cfg.get("inference") or {}
+        if inf.get("name") in INFERENCE_REGISTRY:
+            vbn.set_inference_method(inf["name"], **(inf.get("params") or {}))
+        smp = cfg.get("sampling") or {}
+        if smp.get("name") in SAMPLING_REGISTRY:
+            vbn.set_sampling_method(smp["name"], **(smp.get("params") or {}))
+        return vbn
+
+    @classmethod
+    def from_reference(cls, ref_vbn, device: str = "cuda") -> "VBN":
+        """Snapshot a fitted reference VBN (duck-typed; the reference is not imported)."""
+        return cls(model_from_vbn(ref_vbn), seed=getattr(ref_vbn, "seed", None), device=device)
+
+    def to_device(self, device) -> None:
+        self.device = torch.device(device)
+
+    # ---- configuration ------------------------------------------------------------------
+    def set_inference_method(self, method, **kwargs):
+        name, params = _resolve(method, INFERENCE_REGISTRY, "inference", kwargs)
+        if callable(name) and not isinstance(name, str):
+            self._inference = name
+            self._inference_config = {"callable": True, "name": getattr(name, "__qualname__", str(name))}
+            return
+        self._inference = INFERENCE_REGISTRY[name](**params)
+        self._inference_config = {"name": name, "params": params}
+
+    def set_sampling_method(self, method, **kwargs):
+        name, params = _resolve(method, SAMPLING_REGISTRY, "sampling", kwargs)
+        if callable(name) and not isinstance(name, str):
+            self._sampling = name
+            self._sampling_config = {"callable": True, "name": getattr(name, "__qualname__", str(name))}
+            return
+        self._sampling = SAMPLING_REGISTRY[name](**params)
+        self._sampling_config = {"name": name, "params": params}
+
+    # ---- inference / sampling -----------------------------------------------------------
+    def infer_posterior(self, query, **kwargs):
+        if self._inference is None:
+            raise RuntimeError("Call set_inference_method(...) before infer_posterior().")
+        q = self._normalize_query(query)
+        pdf, samples = self._inference.infer_posterior(self, q, **kwargs)
+        return pdf.detach(), samples.detach()
+
+    def sample(self, query, n_samples: int = 200, **kwargs):
+        if self._sampling is None:
+            raise RuntimeError("Call set_sampling_method(...) before sample().")
+        q = self._normalize_query(query)
+        out = self._sampling.sample(self, q, n_samples=n_samples, **kwargs)
+        if isinstance(out, dict):
+            return {k: v.detach() for k, v in out.items()}
+        return out.detach()
+
+    def _tensor(self, v) -> torch.Tensor:
+        t = v.to(device=self.device, dtype=torch.float32) if isinstance(v, torch.Tensor) else \
+            torch.tensor(v, device=self.device, dtype=torch.float32)
+        if t.dim() == 1:
+            return t.unsqueeze(-1)
+        if t.dim() == 2:
+            return t
+        raise ValueError(f"Expected 1D or 2D tensor, got shape {tuple(t.shape)}")
+
+    def _normalize_query(self, query) -> Query:
+        """reference vbn.py:579-618 (same checks, same messages)."""
+        if isinstance(query, dict):
+            target = query.get("target") or query.get("target_feature")
+            if target is None:
+                raise ValueError("query must contain 'target'")
+            ev_src = query.get("evidence") or {}
+            do_src = query.get("do") or {}
+        elif hasattr(query, "target") and hasattr(query, "evidence"):
+            target, ev_src, do_src = query.target, query.evidence or {}, getattr(query, "do", None) or {}
+        else:
+            raise TypeError("query must be a dict or Query")
+        evidence = {k: self._tensor(v) for k, v in ev_src.items()}
+        do = {k: self._tensor(v) for k, v in do_src.items()}
+        nodes = set(self.model.nodes)
+        if target not in nodes:
+            raise ValueError(f"Unknown target node '{target}'.")
+        unknown = (set(evidence) | set(do)) - nodes
+        if unknown:
+            raise ValueError(f"Unknown query nodes: {sorted(unknown)}")
+        overlap = set(evidence) & set(do)
+        if overlap:
+            raise ValueError(f"Nodes cannot be in both evidence and do: {sorted(overlap)}")
+        infer_batch_size(evidence, do)
+        return Query(target=target, evidence=evidence, do=do)

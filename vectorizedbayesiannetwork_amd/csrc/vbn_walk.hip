@@ -1,0 +1,879 @@
+// vbn_walk.hip — gfx950 (MI355X) particle walk for batched Bayesian-network inference.
+//
+// One wave64 owns 64 particles (lane == particle in every per-particle stage).  The wave
+// walks the plan's topological steps; each node's value lives in LDS (vals[slot][64]), so
+// the [B,S,sum(D)] particle tensor of the reference never touches HBM: only evidence in,
+// pdf/log-weights and the target slice out.
+//
+// NN CPDs (gaussian_nn, mdn, softmax_nn; MLP in->32->32->out): the 32x32 hidden layer runs
+// on MFMA (v_mfma_f32_32x32x2_f32, exact f32) with the hidden unit on the M axis and the
+// particle on the N axis, two 32-particle groups per wave.  Layer 1 (K = #parents <= few)
+// is computed on VALU directly in the MFMA B-operand layout, the head on VALU from the
+// accumulator layout, combined across lane halves with one v_permlane32_swap per output.
+//
+// Reference ops replaced (file:line in Giovannibriglia/VectorizedBayesianNetwork):
+//   topo loop            vbn/inference/monte_carlo_marginalization.py:60-91,
+//                        importance_sampling.py:56-80, likelihood_weighting.py:41-71,
+//                        vbn/sampling/ancestral.py:26-40
+//   gaussian_nn          vbn/cpds/gaussian_nn.py:215-288
+//   linear_gaussian      vbn/cpds/linear_gaussian.py:163-217
+//   mdn                  vbn/cpds/mdn.py:185-272
+//   kde                  vbn/cpds/kde.py:105-182
+//   softmax_nn           vbn/cpds/softmax_nn.py:581-759
+//   softmax + ESS        importance_sampling.py:82-84, likelihood_weighting.py:75-80
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "vbn_hip.h"
+
+#define WAVE 64
+#define KDE_CHUNKS 16
+#define LOG_2PI_F 1.8378770664093453f
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------------------------------
+// small device helpers
+// ------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ void wave_sync() {
+  // LDS ops of one wave are issued in order; this only stops the compiler from moving
+  // LDS accesses of different lanes across the hand-off point.
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_wave_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+__device__ __forceinline__ float relu_nan(float x) { return x < 0.f ? 0.f : x; }  // torch.relu keeps NaN
+
+template <int ACT>
+__device__ __forceinline__ float act_fn(float x) {
+  if (ACT == VBN_ACT_RELU) return relu_nan(x);
+  if (ACT == VBN_ACT_TANH) return tanhf(x);
+  if (ACT == VBN_ACT_GELU) return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+  return x > 0.f ? x : expm1f(x);  // ELU(alpha=1)
+}
+
+// F.softplus(beta=1, threshold=20) (reference cpds/utils.py:6-7)
+__device__ __forceinline__ float softplus_t(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+// Philox-4x32-10 counter-based RNG.
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+__device__ __forceinline__ float box_muller(uint32_t a, uint32_t b) {
+  const float u1 = (float)((a >> 8) + 1u) * (1.0f / 16777216.0f);  // (0,1]
+  const float u2 = (float)(b >> 8) * (1.0f / 16777216.0f);
+  const float r = __builtin_sqrtf(-2.0f * __logf(u1));
+  return r * __builtin_amdgcn_cosf(u2);                              // cos(2*pi*u2)
+}
+
+struct Draw {
+  float ucat;  // uniform for a categorical / index choice (slot 0)
+  float z;     // standard normal (slot 1)
+  float u;     // uniform (slot 1)
+};
+
+struct Lane {
+  float* vals;   // LDS [n_slots][64]
+  float* scr;    // LDS [max_out][64]
+  int lane;
+  int64_t p;     // particle (clamped)
+  int64_t b;     // query
+  int s;         // sample
+};
+
+__device__ __forceinline__ Draw get_draw(const vbn_walk_args& A, const vbn_step& st, int d,
+                                         const Lane& L) {
+  Draw r;
+  if (A.noise) {
+    const int64_t bq = A.noise_b == 1 ? 0 : L.b;
+    const int64_t stride_slot = (int64_t)A.noise_b * A.n_samples * A.dmax;
+    const int64_t base = ((int64_t)st.noise_idx * 2) * stride_slot +
+                         (bq * A.n_samples + L.s) * A.dmax + d;
+    r.ucat = A.noise[base];
+    r.z = A.noise[base + stride_slot];
+    r.u = r.z;
+    return r;
+  }
+  const uint32_t qkey = (st.flags & VBN_F_SHARED) ? 0u : (uint32_t)(A.q_base + L.b + 1);
+  const uint4 c = make_uint4((uint32_t)L.s, qkey, (uint32_t)(st.node_id * 16 + d),
+                             (uint32_t)A.offset);
+  const uint2 k = make_uint2((uint32_t)A.seed, (uint32_t)(A.seed >> 32) ^ (uint32_t)(A.offset >> 32));
+  const uint4 x = philox4x32(c, k);
+  r.ucat = u01(x.x);
+  r.z = box_muller(x.y, x.z);
+  r.u = u01(x.w);
+  return r;
+}
+
+__device__ __forceinline__ float vread(const Lane& L, int slot) { return L.vals[slot * WAVE + L.lane]; }
+__device__ __forceinline__ void vwrite(const Lane& L, int slot, float v) { L.vals[slot * WAVE + L.lane] = v; }
+
+__device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_step& st, int d,
+                                             const Lane& L) {
+  const int64_t row = A.fixed_per_particle ? L.p : L.b;
+  return A.fixed[row * A.fixed_ld + st.fixed_col + d];
+}
+
+// ------------------------------------------------------------------------------------------
+// MLP (in -> 32 -> 32 -> n_out) for the wave's 64 particles; head outputs to scr[j][lane].
+//
+// Parameter blocks (packed by vectorizedbayesiannetwork_amd/plan.py):
+//   off_std : mean_x[n_in], std_x[n_in]                          (gaussian_nn only)
+//   off_w1  : [half 2][s 16][n_in + 1]  = W1[2s+half][:], b1[2s+half]
+//   off_w2  : [q 4][lane 64][4]        = W2[lane&31][2(4q+e)+(lane>>5)]   (A fragments)
+//   off_b2  : [half 2][r 16]           = b2[row(r, half)]
+//   off_w3  : [j][half 2][r 16]        = W3[j][row(r, half)]
+//   off_b3  : [n_out]
+// with row(r, h) = (r&3) + 8(r>>2) + 4h, the 32x32 MFMA accumulator row of register r.
+// ------------------------------------------------------------------------------------------
+
+template <int ACT, bool STD>
+__device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  const float* __restrict__ P = A.params;
+  const int lane = L.lane;
+  const int half = lane >> 5;
+  const int c = lane & 31;
+  const int nin = st.n_in;
+
+  float h1a[16], h1b[16];
+  const float* w1 = P + st.off_w1 + half * 16 * (nin + 1);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const float bias = w1[s * (nin + 1) + nin];
+    h1a[s] = bias;
+    h1b[s] = bias;
+  }
+  for (int d = 0; d < nin; ++d) {
+    const int slot = A.in_cols[st.in_off + d];
+    float za = L.vals[slot * WAVE + c];
+    float zb = L.vals[slot * WAVE + 32 + c];
+    if (STD) {
+      const float m = P[st.off_std + d];
+      const float sd = P[st.off_std + nin + d];
+      za = (za - m) / sd;
+      zb = (zb - m) / sd;
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const float w = w1[s * (nin + 1) + d];
+      h1a[s] = fmaf(w, za, h1a[s]);
+      h1b[s] = fmaf(w, zb, h1b[s]);
+    }
+  }
+
+  float w2[16];
+  const float4* w2p = reinterpret_cast<const float4*>(P + st.off_w2);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = w2p[q * WAVE + lane];
+    w2[4 * q + 0] = v.x;
+    w2[4 * q + 1] = v.y;
+    w2[4 * q + 2] = v.z;
+    w2[4 * q + 3] = v.w;
+  }
+  f32x16 acc0, acc1;
+  const float* b2 = P + st.off_b2 + half * 16;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc0[r] = b2[r];
+    acc1[r] = b2[r];
+  }
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[s], act_fn<ACT>(h1a[s]), acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[s], act_fn<ACT>(h1b[s]), acc1, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    acc0[r] = act_fn<ACT>(acc0[r]);
+    acc1[r] = act_fn<ACT>(acc1[r]);
+  }
+
+  const int nout = st.n_out;
+  for (int j = 0; j < nout; ++j) {
+    const float4* w3 = reinterpret_cast<const float4*>(P + st.off_w3 + (j * 2 + half) * 16);
+    float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 w = w3[q];
+      p0 = fmaf(w.x, acc0[4 * q + 0], p0);
+      p1 = fmaf(w.x, acc1[4 * q + 0], p1);
+      p0 = fmaf(w.y, acc0[4 * q + 1], p0);
+      p1 = fmaf(w.y, acc1[4 * q + 1], p1);
+      p0 = fmaf(w.z, acc0[4 * q + 2], p0);
+      p1 = fmaf(w.z, acc1[4 * q + 2], p1);
+      p0 = fmaf(w.w, acc0[4 * q + 3], p0);
+      p1 = fmaf(w.w, acc1[4 * q + 3], p1);
+    }
+    // lanes 0-31 take group 0's two halves, lanes 32-63 group 1's: one swap.
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0), __float_as_uint(p1), false, false);
+    const float out = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    L.scr[j * WAVE + lane] = out + P[st.off_b3 + j];
+  }
+  wave_sync();
+}
+
+__device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  const bool sd = (st.flags & VBN_F_STANDARDIZE) != 0;
+  switch (st.act * 2 + (sd ? 1 : 0)) {
+    case 0: mlp_forward<VBN_ACT_RELU, false>(A, st, L); break;
+    case 1: mlp_forward<VBN_ACT_RELU, true>(A, st, L); break;
+    case 2: mlp_forward<VBN_ACT_TANH, false>(A, st, L); break;
+    case 3: mlp_forward<VBN_ACT_TANH, true>(A, st, L); break;
+    case 4: mlp_forward<VBN_ACT_GELU, false>(A, st, L); break;
+    case 5: mlp_forward<VBN_ACT_GELU, true>(A, st, L); break;
+    case 6: mlp_forward<VBN_ACT_ELU, false>(A, st, L); break;
+    default: mlp_forward<VBN_ACT_ELU, true>(A, st, L); break;
+  }
+}
+
+// value of node dim d for this particle: fresh draw result or fixed input
+#define NODE_X(d) (vread(L, st.out_col + (d)))
+
+// ------------------------------------------------------------------------------------------
+// gaussian_nn (gaussian_nn.py:215-288)
+//   tail (non-root): std_y[D], mean_y[D], min_scale
+//   tail (root)    : loc[D], scale[D], log_scale[D]
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
+#pragma clang fp contract(off)
+  const float* __restrict__ P = A.params;
+  const int D = st.out_dim;
+  const bool latent = st.role == VBN_ROLE_LATENT;
+  const bool want_lp = (st.flags & VBN_F_LOGP) != 0;
+  const float* t = P + st.off_tail;
+  if (st.flags & VBN_F_ROOT) {
+    for (int d = 0; d < D; ++d) {
+      const float loc = t[d], scale = t[D + d];
+      float x;
+      if (latent) {
+        const Draw r = get_draw(A, st, d, L);
+        x = r.z * scale + loc;                       // torch.normal(loc, scale)
+        vwrite(L, st.out_col + d, x);
+      } else {
+        x = fixed_value(A, st, d, L);
+        vwrite(L, st.out_col + d, x);
+      }
+      if (want_lp) {                                 // Normal.log_prob (gaussian_nn.py:276-279)
+        const float diff = x - loc;
+        lp += -(diff * diff) / (2.0f * (scale * scale)) - t[2 * D + d] - 0.91893853320467274178f;
+      }
+    }
+    return;
+  }
+  run_mlp(A, st, L);
+  const float min_scale = t[2 * D];
+  float acc = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float o_loc = L.scr[d * WAVE + L.lane];
+    const float o_sc = L.scr[(D + d) * WAVE + L.lane];
+    const float sy = t[d], my = t[D + d];
+    const float loc = o_loc * sy + my;
+    const float scale = (softplus_t(o_sc) + min_scale) * sy;
+    float x;
+    if (latent) {
+      const Draw r = get_draw(A, st, d, L);
+      x = loc + r.z * scale;
+    } else {
+      x = fixed_value(A, st, d, L);
+    }
+    vwrite(L, st.out_col + d, x);
+    if (want_lp) {
+      const float diff = x - loc;
+      acc += (diff * diff) / (scale * scale) + 2.0f * logf(scale) + LOG_2PI_F;
+    }
+  }
+  if (want_lp) lp += -0.5f * acc;
+}
+
+// ------------------------------------------------------------------------------------------
+// linear_gaussian (linear_gaussian.py:163-217)
+//   tail: W[D][n_in] (W[:, d] of the reference's [n_in, D]), bias[D], scale[D], log_scale[D]
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void step_linear_gaussian(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
+#pragma clang fp contract(off)
+  const float* __restrict__ P = A.params;
+  const int D = st.out_dim, nin = st.n_in;
+  const float* t = P + st.off_tail;
+  const float* W = t;
+  const float* bias = t + D * nin;
+  const float* scale = bias + D;
+  const float* log_scale = scale + D;
+  const bool latent = st.role == VBN_ROLE_LATENT;
+  float acc = 0.f;
+  for (int d = 0; d < D; ++d) {
+    float mu = 0.f;
+    for (int i = 0; i < nin; ++i) mu = fmaf(vread(L, A.in_cols[st.in_off + i]), W[d * nin + i], mu);
+    const float loc = (nin > 0) ? mu + bias[d] : bias[d];
+    float x;
+    if (latent) {
+      const Draw r = get_draw(A, st, d, L);
+      x = loc + r.z * scale[d];
+    } else {
+      x = fixed_value(A, st, d, L);
+    }
+    vwrite(L, st.out_col + d, x);
+    if (st.flags & VBN_F_LOGP) {
+      const float diff = x - loc;
+      acc += (diff * diff) / (scale[d] * scale[d]) + 2.0f * log_scale[d] + LOG_2PI_F;
+    }
+  }
+  if (st.flags & VBN_F_LOGP) lp += -0.5f * acc;
+}
+
+// ------------------------------------------------------------------------------------------
+// categorical inverse-CDF: smallest k with cumsum(p)[k] > u * sum(p)
+// ------------------------------------------------------------------------------------------
+template <typename F>
+__device__ __forceinline__ int inv_cdf(int K, float u, F prob) {
+  float tot = 0.f;
+  for (int k = 0; k < K; ++k) tot += prob(k);
+  const float thr = u * tot;
+  float cum = 0.f;
+  int idx = K - 1;
+  for (int k = 0; k < K - 1; ++k) {
+    cum += prob(k);
+    if (cum > thr) { idx = k; break; }
+  }
+  return idx;
+}
+
+// ------------------------------------------------------------------------------------------
+// mdn (mdn.py:185-272)
+//   non-root: scr = [logits K][comp k: loc D, raw_scale D];  tail: min_scale
+//   root    : tail = pi[K], log_pi[K], loc[K*D], scale[K*D], log_scale[K*D], var[K*D]
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
+#pragma clang fp contract(off)
+  const float* __restrict__ P = A.params;
+  const int D = st.out_dim, K = st.k;
+  const float* t = P + st.off_tail;
+  const bool root = (st.flags & VBN_F_ROOT) != 0;
+  const bool latent = st.role == VBN_ROLE_LATENT;
+  const bool want_lp = (st.flags & VBN_F_LOGP) != 0;
+  const int lane = L.lane;
+  float* scr = L.scr;
+  float min_scale = 0.f, lmax = 0.f, lsum = 1.f, psum = 1.f;
+  if (!root) {
+    run_mlp(A, st, L);
+    min_scale = t[0];
+    // pi = softmax(logits).clamp_min(1e-5); pi /= sum (mdn.py:227-228)
+    lmax = -INFINITY;
+    for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, scr[k * WAVE + lane]);
+    lsum = 0.f;
+    for (int k = 0; k < K; ++k) lsum += expf(scr[k * WAVE + lane] - lmax);
+    psum = 0.f;
+    for (int k = 0; k < K; ++k) psum += fmaxf(expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f);
+    psum = fmaxf(psum, 1e-12f);
+  }
+  auto pi_k = [&](int k) -> float {
+    if (root) return t[k];
+    return fmaxf(expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f) / psum;
+  };
+  auto loc_kd = [&](int k, int d) -> float {
+    return root ? t[2 * K + k * D + d] : scr[(K + k * 2 * D + d) * WAVE + lane];
+  };
+  auto scale_kd = [&](int k, int d) -> float {
+    return root ? t[2 * K + K * D + k * D + d]
+                : softplus_t(scr[(K + k * 2 * D + D + d) * WAVE + lane]) + min_scale;
+  };
+  if (latent) {
+    const Draw r0 = get_draw(A, st, 0, L);
+    const int idx = inv_cdf(K, r0.ucat, pi_k);
+    for (int d = 0; d < D; ++d) {
+      const Draw r = d == 0 ? r0 : get_draw(A, st, d, L);
+      vwrite(L, st.out_col + d, loc_kd(idx, d) + r.z * scale_kd(idx, d));
+    }
+  } else {
+    for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
+  }
+  if (want_lp) {
+    // logsumexp_k(log pi_k + log N_k(x))  (mdn.py:263-272), online form
+    float m = -INFINITY, se = 0.f;
+    for (int k = 0; k < K; ++k) {
+      float acc = 0.f;
+      for (int d = 0; d < D; ++d) {
+        const float x = NODE_X(d);
+        float ls, var;
+        if (root) {
+          ls = t[2 * K + 2 * K * D + k * D + d];
+          var = t[2 * K + 3 * K * D + k * D + d];
+        } else {
+          ls = logf(scale_kd(k, d));
+          var = expf(2.0f * ls);
+        }
+        const float diff = x - loc_kd(k, d);
+        acc += (diff * diff) / var + 2.0f * ls + LOG_2PI_F;
+      }
+      const float lpi = root ? t[K + k] : logf(pi_k(k));
+      const float term = lpi + (-0.5f * acc);
+      if (term == -INFINITY) continue;
+      if (term > m) {
+        se = se * expf(m - term) + 1.0f;
+        m = term;
+      } else {
+        se += expf(term - m);
+      }
+    }
+    lp += (m == -INFINITY) ? m : m + logf(se);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// softmax_nn (softmax_nn.py:581-759)
+//   scr (non-root) = logits[D][C];  root logits table at off_pts ([D][C], already log_softmax'd)
+//   tail: edges[D][C+1], sample_values[D][C], class_values[D][C], within_scale, min_bw, min_bw2
+//   aux0 = within-bin mode, aux1 = discrete-dim bit mask
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
+#pragma clang fp contract(off)
+  const float* __restrict__ P = A.params;
+  const int D = st.out_dim, C = st.k;
+  const float* t = P + st.off_tail;
+  const float* edges = t;
+  const float* svals = t + D * (C + 1);
+  const float* cvals = svals + D * C;
+  const float wscale = cvals[D * C + 0];
+  const float min_bw = cvals[D * C + 1];
+  const float min_bw2 = cvals[D * C + 2];
+  const bool root = (st.flags & VBN_F_ROOT) != 0;
+  const bool latent = st.role == VBN_ROLE_LATENT;
+  const bool clip = (st.flags & VBN_F_CLIP) != 0;
+  const int mode = st.aux0;
+  const int lane = L.lane;
+  if (!root) run_mlp(A, st, L);
+  float lp_acc = 0.f;
+  for (int d = 0; d < D; ++d) {
+    auto logit = [&](int c) -> float {
+      return root ? P[st.off_pts + d * C + c] : L.scr[(d * C + c) * WAVE + lane];
+    };
+    float m = -INFINITY;
+    for (int c = 0; c < C; ++c) m = fmaxf(m, logit(c));
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += expf(logit(c) - m);
+    const bool disc = (st.aux1 >> d) & 1;
+    const float* e = edges + d * (C + 1);
+    float x;
+    int idx;
+    if (latent) {
+      const Draw r = get_draw(A, st, d, L);
+      idx = inv_cdf(C, r.ucat, [&](int c) { return expf(logit(c) - m) / se; });
+      const float left = e[idx];
+      const float right = e[idx + 1 < C ? idx + 1 : C];
+      const float width = fmaxf(right - left, min_bw);
+      const float center = 0.5f * (left + right);
+      if (disc) {
+        x = svals[d * C + idx];
+      } else {
+        float cont;
+        if (mode == VBN_WITHIN_UNIFORM) {
+          cont = left + r.u * width;
+        } else if (mode == VBN_WITHIN_TRIANGULAR) {
+          const float lv = left + width * sqrtf(fmaxf(r.u * 0.5f, 0.0f));
+          const float rv = right - width * sqrtf(fmaxf((1.0f - r.u) * 0.5f, 0.0f));
+          cont = r.u < 0.5f ? lv : rv;
+        } else {
+          cont = center + r.z * fmaxf(wscale * width, min_bw);
+        }
+        if (clip) cont = fminf(fmaxf(cont, left), right);
+        x = cont;
+      }
+    } else {
+      x = fixed_value(A, st, d, L);
+    }
+    vwrite(L, st.out_col + d, x);
+    if (st.flags & VBN_F_LOGP) {
+      // bin: count(x >= edges) - 1 clamped (bit-exact); discrete: first exact class match
+      int bin;
+      if (disc) {
+        bin = 0;
+        for (int c = C - 1; c >= 0; --c)
+          if (x == cvals[d * C + c]) bin = c;
+      } else {
+        int cnt = 0;
+        for (int c = 0; c <= C; ++c) cnt += (x >= e[c]) ? 1 : 0;
+        bin = min(max(cnt - 1, 0), C - 1);
+      }
+      const float log_bin = logit(bin) - m - logf(se);
+      float lw = 0.f;
+      if (!disc) {
+        const float left = e[bin];
+        const float right = e[bin + 1 < C ? bin + 1 : C];
+        const float width = fmaxf(right - left, min_bw);
+        const float center = 0.5f * (left + right);
+        const float xu = clip ? fminf(fmaxf(x, left), right) : x;
+        const bool inside = (x >= left) && (x <= right);
+        if (mode == VBN_WITHIN_UNIFORM) {
+          lw = -logf(width);
+          if (!clip && !inside) lw = -INFINITY;
+        } else if (mode == VBN_WITHIN_TRIANGULAR) {
+          const float dl = fmaxf(width * (center - left), min_bw2);
+          const float dr = fmaxf(width * (right - center), min_bw2);
+          float pdf = (xu <= center) ? 2.0f * (xu - left) / dl : 2.0f * (right - xu) / dr;
+          pdf = fmaxf(pdf, 0.0f);
+          lw = logf(fmaxf(pdf, 1e-12f));
+          if (!clip && !inside) lw = -INFINITY;
+        } else {
+          const float sigma = fmaxf(wscale * width, min_bw);
+          const float diff = xu - center;
+          lw = -(diff * diff) / (2.0f * (sigma * sigma)) - logf(sigma) - 0.91893853320467274178f;
+        }
+      }
+      lp_acc += log_bin + lw;
+    }
+  }
+  if (st.flags & VBN_F_LOGP) lp += lp_acc;
+}
+
+// ------------------------------------------------------------------------------------------
+// kde (kde.py:105-182)
+//   points at off_pts: [M][stride] = parents[dp] ++ targets[D]
+//   tail: inv_sp, inv_sy, noise_scale, cy, log_n;  aux0 = dp, aux1 = stride
+// Weights are taken relative to the kernel's peak (exp(-q/2) <= 1); if every weight of a
+// particle underflows the pass is redone relative to the particle's nearest point.
+// ------------------------------------------------------------------------------------------
+// squared scaled distance to point ``pt`` over the parent dims.  DP >= 0: parent values in
+// registers (pv); DP < 0: generic count, parent values re-read from LDS.
+template <int DP>
+__device__ __forceinline__ float kde_qp(const float* __restrict__ pt, const float (&pv)[4], float inv,
+                                        int dp, const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  float q = 0.f;
+  if (DP >= 0) {
+#pragma unroll
+    for (int i = 0; i < (DP >= 0 ? DP : 0); ++i) {
+      const float df = (pv[i] - pt[i]) * inv;
+      q = fmaf(df, df, q);
+    }
+  } else {
+    for (int i = 0; i < dp; ++i) {
+      const float df = (vread(L, A.in_cols[st.in_off + i]) - pt[i]) * inv;
+      q = fmaf(df, df, q);
+    }
+  }
+  return q;
+}
+
+template <int DY>
+__device__ __forceinline__ float kde_qy(const float* __restrict__ pty, float x0, float inv, int D,
+                                        const vbn_step& st, const Lane& L) {
+  if (DY == 1) {
+    const float df = (x0 - pty[0]) * inv;
+    return df * df;
+  }
+  float q = 0.f;
+  for (int d = 0; d < D; ++d) {
+    const float df = (vread(L, st.out_col + d) - pty[d]) * inv;
+    q = fmaf(df, df, q);
+  }
+  return q;
+}
+
+template <int DP, int DY>
+__device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
+#pragma clang fp contract(off)
+  const float* __restrict__ P = A.params;
+  const float* __restrict__ pts = P + st.off_pts;
+  const int M = st.k, dp = DP >= 0 ? DP : st.aux0, stride = st.aux1, D = DY > 0 ? DY : st.out_dim;
+  const float* t = P + st.off_tail;
+  const float inv_sp = t[0], inv_sy = t[1], noise_scale = t[2], cy = t[3], log_n = t[4];
+  const bool root = (st.flags & VBN_F_ROOT) != 0;
+  const int lane = L.lane;
+  float pv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < (DP > 0 ? DP : 0); ++i) pv[i] = vread(L, A.in_cols[st.in_off + i]);
+
+  if (st.role == VBN_ROLE_LATENT) {
+    const Draw r0 = get_draw(A, st, 0, L);
+    int idx;
+    if (root) {
+      idx = min((int)(r0.ucat * (float)M), M - 1);          // randint(0, M)
+    } else {
+      // pass 1: per-chunk weight sums -> scr[chunk][lane]
+      const int csz = (M + KDE_CHUNKS - 1) / KDE_CHUNKS;
+      double tot = 0.0;
+      float qmin = INFINITY;
+      for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+        const int j0 = ch * csz, j1 = min(M, j0 + csz);
+        float cs = 0.f;
+        for (int j = j0; j < j1; ++j) {
+          const float q = kde_qp<DP>(pts + (int64_t)j * stride, pv, inv_sp, dp, A, st, L);
+          qmin = fminf(qmin, q);
+          cs += __expf(-0.5f * q);
+        }
+        L.scr[ch * WAVE + lane] = cs;
+        tot += (double)cs;
+      }
+      float shift = 0.f;
+      if (!(tot > 0.0)) {                                 // all weights underflowed
+        shift = qmin;
+        tot = 0.0;
+        for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+          const int j0 = ch * csz, j1 = min(M, j0 + csz);
+          float cs = 0.f;
+          for (int j = j0; j < j1; ++j)
+            cs += __expf(-0.5f * (kde_qp<DP>(pts + (int64_t)j * stride, pv, inv_sp, dp, A, st, L) - shift));
+          L.scr[ch * WAVE + lane] = cs;
+          tot += (double)cs;
+        }
+      }
+      // pass 2: locate the chunk, then scan inside it (per-lane chunk; vector loads)
+      const double thr = (double)r0.ucat * tot;
+      double cum = 0.0;
+      int ch = KDE_CHUNKS - 1;
+      for (int c2 = 0; c2 < KDE_CHUNKS; ++c2) {
+        const double nx = cum + (double)L.scr[c2 * WAVE + lane];
+        if (nx > thr) { ch = c2; break; }
+        cum = nx;
+      }
+      const int j0 = ch * csz, j1 = min(M, j0 + csz);
+      const float rem = (float)(thr - cum);
+      float cs = 0.f;
+      idx = max(j1 - 1, 0);
+      for (int j = j0; j < j1; ++j) {
+        cs += __expf(-0.5f * (kde_qp<DP>(pts + (int64_t)j * stride, pv, inv_sp, dp, A, st, L) - shift));
+        if (cs > rem) { idx = j; break; }
+      }
+      wave_sync();
+    }
+    for (int d = 0; d < D; ++d) {
+      const Draw r = d == 0 ? r0 : get_draw(A, st, d, L);
+      const float sel = pts[(int64_t)idx * stride + dp + d];
+      vwrite(L, st.out_col + d, sel + r.z * noise_scale);
+    }
+  } else {
+    for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
+  }
+
+  if (st.flags & VBN_F_LOGP) {
+    const float x0 = NODE_X(0);
+    float sy = 0.f, sp = 0.f, qymin = INFINITY, qpmin = INFINITY, qsmin = INFINITY;
+    for (int j = 0; j < M; ++j) {
+      const float* pt = pts + (int64_t)j * stride;
+      const float qy = kde_qy<DY>(pt + dp, x0, inv_sy, D, st, L);
+      if (root) {
+        sy += __expf(-0.5f * qy);
+        qymin = fminf(qymin, qy);
+      } else {
+        const float qp = kde_qp<DP>(pt, pv, inv_sp, dp, A, st, L);
+        sp += __expf(-0.5f * qp);
+        sy += __expf(-0.5f * (qp + qy));
+        qpmin = fminf(qpmin, qp);
+        qsmin = fminf(qsmin, qp + qy);
+      }
+    }
+    float sh_y = 0.f, sh_p = 0.f;
+    if (!(sy > 0.f) || (!root && !(sp > 0.f))) {   // underflow: re-sum relative to the minimum
+      sh_y = root ? qymin : qsmin;
+      sh_p = qpmin;
+      sy = 0.f;
+      sp = 0.f;
+      for (int j = 0; j < M; ++j) {
+        const float* pt = pts + (int64_t)j * stride;
+        const float qy = kde_qy<DY>(pt + dp, x0, inv_sy, D, st, L);
+        if (root) {
+          sy += __expf(-0.5f * (qy - sh_y));
+        } else {
+          const float qp = kde_qp<DP>(pt, pv, inv_sp, dp, A, st, L);
+          sp += __expf(-0.5f * (qp - sh_p));
+          sy += __expf(-0.5f * (qp + qy - sh_y));
+        }
+      }
+    }
+    const float ls_y = logf(sy) - 0.5f * sh_y;
+    if (root) {
+      lp += ls_y + cy - log_n;
+    } else {
+      const float ls_p = logf(sp) - 0.5f * sh_p;
+      lp += (ls_y - ls_p) + cy;
+    }
+  }
+}
+
+__device__ __forceinline__ void step_kde(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
+  if (st.out_dim == 1) {
+    switch (st.aux0) {
+      case 0: step_kde_t<0, 1>(A, st, L, lp); return;
+      case 1: step_kde_t<1, 1>(A, st, L, lp); return;
+      case 2: step_kde_t<2, 1>(A, st, L, lp); return;
+      case 3: step_kde_t<3, 1>(A, st, L, lp); return;
+      default: break;
+    }
+  }
+  step_kde_t<-1, -1>(A, st, L, lp);
+}
+
+// ------------------------------------------------------------------------------------------
+// the walk
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(WAVE) vbn_walk_kernel(const vbn_walk_args A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  Lane L;
+  L.lane = threadIdx.x;
+  L.vals = smem;
+  L.scr = smem + A.n_slots * WAVE;
+  const int64_t total = A.n_queries * (int64_t)A.n_samples;
+  const int64_t p_raw = (int64_t)blockIdx.x * WAVE + L.lane;
+  const bool valid = p_raw < total;
+  L.p = valid ? p_raw : total - 1;
+  L.b = L.p / A.n_samples;
+  L.s = (int)(L.p - L.b * A.n_samples);
+
+  float lp = 0.f;
+  for (int i = 0; i < A.n_steps; ++i) {
+    const vbn_step st = A.steps[i];
+    if (st.role == VBN_ROLE_SKIP) continue;
+    if (st.role == VBN_ROLE_FIXED && !(st.flags & VBN_F_LOGP)) {   // evidence / do: value only
+      for (int d = 0; d < st.out_dim; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
+      wave_sync();
+      continue;
+    }
+    switch (st.kind) {
+      case VBN_KIND_GAUSSIAN_NN: step_gaussian_nn(A, st, L, lp); break;
+      case VBN_KIND_LINEAR_GAUSSIAN: step_linear_gaussian(A, st, L, lp); break;
+      case VBN_KIND_MDN: step_mdn(A, st, L, lp); break;
+      case VBN_KIND_KDE: step_kde(A, st, L, lp); break;
+      default: step_softmax_nn(A, st, L, lp); break;
+    }
+    wave_sync();
+  }
+  if (!valid) return;
+  if (A.out_lp && A.mode != VBN_MODE_SAMPLE) A.out_lp[L.p] = (A.mode == VBN_MODE_MCM) ? expf(lp) : lp;
+  if (A.out_x) {
+    for (int k = 0; k < A.n_out_cols; ++k)
+      A.out_x[L.p * A.n_out_cols + k] = vread(L, A.out_cols[k]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// per-query weight normalisation (softmax over S + ESS, or max-shifted exp)
+// ------------------------------------------------------------------------------------------
+#define NW_THREADS 256
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__global__ void __launch_bounds__(NW_THREADS) vbn_normalize_kernel(const float* log_w, float* w, float* ess,
+                                                                  int S, int normalize, float eps) {
+  __shared__ float red[NW_THREADS / WAVE];
+  __shared__ int nan_flag;
+  const int64_t row = blockIdx.x;
+  const float* x = log_w + row * S;
+  float* y = w + row * S;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  if (tid == 0) nan_flag = 0;
+  __syncthreads();
+  float m = -INFINITY;
+  int has_nan = 0;
+  for (int i = tid; i < S; i += NW_THREADS) {
+    const float v = x[i];
+    has_nan |= (v != v);
+    m = fmaxf(m, v);
+  }
+  if (has_nan) atomicOr(&nan_flag, 1);
+  m = wave_max(m);
+  if (lane == 0) red[wid] = m;
+  __syncthreads();
+  m = red[0];
+  for (int k = 1; k < NW_THREADS / WAVE; ++k) m = fmaxf(m, red[k]);
+  const bool row_nan = nan_flag != 0;
+  __syncthreads();
+  if (!normalize) {
+    for (int i = tid; i < S; i += NW_THREADS) {
+      const float v = expf(x[i] - m);                // all -inf row: exp(NaN) stays NaN
+      y[i] = row_nan ? NAN : (v != v ? v : fmaxf(v, eps));
+    }
+    return;
+  }
+  float sum = 0.f;
+  for (int i = tid; i < S; i += NW_THREADS) sum += expf(x[i] - m);
+  sum = wave_sum(sum);
+  if (lane == 0) red[wid] = sum;
+  __syncthreads();
+  sum = 0.f;
+  for (int k = 0; k < NW_THREADS / WAVE; ++k) sum += red[k];
+  __syncthreads();
+  float sq = 0.f;
+  for (int i = tid; i < S; i += NW_THREADS) {
+    const float v = row_nan ? NAN : expf(x[i] - m) / sum;   // all -inf row: (-inf)-(-inf) -> NaN
+    y[i] = v;
+    sq += v * v;
+  }
+  sq = wave_sum(sq);
+  if (lane == 0) red[wid] = sq;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+    for (int k = 0; k < NW_THREADS / WAVE; ++k) t += red[k];
+    if (ess) ess[row] = 1.0f / t;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// C-ABI
+// ------------------------------------------------------------------------------------------
+static thread_local char g_err[512];
+
+static int fail(int code, const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+
+extern "C" int vbn_hip_abi_version(void) { return VBN_ABI_VERSION; }
+extern "C" const char* vbn_hip_last_error(void) { return g_err; }
+
+extern "C" int64_t vbn_hip_lds_bytes(int32_t n_slots, int32_t max_out) {
+  const int32_t scr = max_out > KDE_CHUNKS ? max_out : KDE_CHUNKS;
+  return (int64_t)(n_slots + scr) * WAVE * (int64_t)sizeof(float);
+}
+
+extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
+  if (!a || !a->steps || !a->params || a->n_samples <= 0 || a->n_queries <= 0 || a->n_slots <= 0)
+    return fail(VBN_E_ARGS, "vbn_hip_walk: bad arguments");
+  if (a->out_x && (!a->out_cols || a->n_out_cols <= 0))
+    return fail(VBN_E_ARGS, "vbn_hip_walk: out_x without out_cols");
+  const int64_t lds = vbn_hip_lds_bytes(a->n_slots, a->max_out);
+  if (lds > 160 * 1024) return fail(VBN_E_LDS, "vbn_hip_walk: plan needs more than 160 KiB of LDS per wave");
+  const int64_t total = a->n_queries * (int64_t)a->n_samples;
+  const int64_t blocks = (total + WAVE - 1) / WAVE;
+  if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
+  hipLaunchKernelGGL(vbn_walk_kernel, dim3((unsigned)blocks), dim3(WAVE), (size_t)lds,
+                     (hipStream_t)stream, *a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  return 0;
+}
+
+extern "C" int vbn_hip_normalize_weights(const float* log_w, float* w, float* ess, int64_t n_queries,
+                                         int32_t n_samples, int32_t normalize, float eps, void* stream) {
+  if (!log_w || !w || n_queries <= 0 || n_samples <= 0)
+    return fail(VBN_E_ARGS, "vbn_hip_normalize_weights: bad arguments");
+  hipLaunchKernelGGL(vbn_normalize_kernel, dim3((unsigned)n_queries), dim3(NW_THREADS), 0,
+                     (hipStream_t)stream, log_w, w, ess, n_samples, normalize, eps);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  return 0;
+}

@@ -1,0 +1,379 @@
+"""Accelerated engines with the reference's plugin protocol.
+
+Each class follows the reference engine contract (reference ``core/base.py:94-101``):
+``cls(**params)`` then ``infer_posterior(vbn, query, **kw) -> (pdf[B,S], samples[B,S,Dt])``
+or ``sample(vbn, query, n_samples, **kw)``; ``vbn`` is read duck-typed (``vbn.dag``,
+``vbn.nodes``, ``vbn.device``), so the classes work with this package's :class:`VBN` and
+can be registered into the reference's own ``INFERENCE_REGISTRY``.
+
+Semantics mirror the reference branch by branch:
+
+* MCM (monte_carlo_marginalization.py:18-92): do-target -> pdf = 1; all target parents
+  observed -> only the target is walked (root target gives ``(1,S)``); otherwise the full
+  walk, pdf = p(target | sampled parents), evidence not weighted; root draws shared by
+  all queries.
+* IS (importance_sampling.py:24-93): per-query root draws, evidence log-weights, softmax
+  over S, ESS, batch-global fallback to LW when any ESS < max(1, 0.1*S) (NaN never triggers).
+* LW (likelihood_weighting.py:24-82): evidence clamped (nan->0, +-1e6), shared root draws,
+  softmax or max-shifted exp.
+* ancestral (sampling/ancestral.py:13-65): the walk without weights; target slice or all nodes.
+
+RNG: counter-based Philox keyed by ``(seed, offset, node, query, sample)``.  The seed of a
+call is taken from the global torch generator (so ``torch.manual_seed`` makes runs
+repeatable, and the reference's "batch row 0 == single query" property holds for IS).
+For parity tests the draws can be injected (``_noise=``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import ops
+from .model import BNModel, model_from_vbn
+from .plan import (MODE_MCM, MODE_SAMPLE, MODE_WEIGHTED, PackedModel, QueryPlan, barren_pruned,
+                   build_plan)
+from .registry import register_inference, register_sampling
+
+__all__ = [
+    "Query",
+    "MonteCarloMarginalization",
+    "ImportanceSampling",
+    "LikelihoodWeighting",
+    "AncestralSampler",
+    "infer_batch_size",
+]
+
+
+@dataclass
+class Query:
+    """Inference/sampling query (reference core/base.py:18-25)."""
+
+    target: Optional[str]
+    evidence: Dict[str, torch.Tensor]
+    do: Dict[str, torch.Tensor] = field(default_factory=dict)
+
+
+def infer_batch_size(evidence: Dict, do: Optional[Dict] = None) -> int:
+    """reference utils/__init__.py:46-61"""
+    evidence = evidence or {}
+    do = do or {}
+    if evidence:
+        b = int(next(iter(evidence.values())).shape[0])
+        if do and int(next(iter(do.values())).shape[0]) != b:
+            raise ValueError("Evidence and do batch sizes must match.")
+        return b
+    if do:
+        return int(next(iter(do.values())).shape[0])
+    return 1
+
+
+def _as2d(x: torch.Tensor) -> torch.Tensor:
+    if x.dim() == 1:
+        return x.unsqueeze(-1)
+    if x.dim() == 2:
+        return x
+    raise ValueError(f"Expected 1D or 2D tensor, got shape {tuple(x.shape)}")
+
+
+def _device_of(vbn) -> torch.device:
+    dev = torch.device(getattr(vbn, "device", "cuda"))
+    if dev.type != "cuda":
+        raise RuntimeError(
+            f"the accelerated engines run on an MI355X; vbn.device is {dev} "
+            "(construct the model with device='cuda' or call vbn.to_device('cuda'))")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def packed_model(vbn, device: torch.device) -> PackedModel:
+    model: BNModel = model_from_vbn(vbn)
+    key = ("packed", str(device), model.version)
+    pk = model._cache.get(key)
+    if pk is None:
+        pk = PackedModel(model, device)
+        model._cache[key] = pk
+    return pk
+
+
+def _plan(pk: PackedModel, key, **kw) -> QueryPlan:
+    ck = ("plan",) + key
+    p = pk.model._cache.get(ck)
+    if p is None:
+        p = build_plan(pk, **kw)
+        pk.model._cache[ck] = p
+    return p
+
+
+def _fixed_values(query, device, clamp: bool = False) -> Dict[str, torch.Tensor]:
+    """prepare_fixed_values (reference inference/_core.py:117-135)."""
+    vals: Dict[str, torch.Tensor] = {}
+    for k, v in (query.do or {}).items():
+        vals[k] = _as2d(torch.as_tensor(v)).to(device=device, dtype=torch.float32)
+    for k, v in (query.evidence or {}).items():
+        v = _as2d(torch.as_tensor(v)).to(device=device, dtype=torch.float32)
+        if clamp:                                             # clamp_evidence (_core.py:112-114)
+            v = torch.nan_to_num(v, nan=0.0, posinf=1e6, neginf=-1e6).clamp(min=-1e6, max=1e6)
+        vals[k] = v
+    return vals
+
+
+def _fixed_buffer(plan: QueryPlan, vals: Dict[str, torch.Tensor], rows: int, device) -> torch.Tensor:
+    if not plan.fixed_nodes:
+        return torch.zeros(rows, 1, device=device, dtype=torch.float32)
+    cols = []
+    for n in plan.fixed_nodes:
+        v = vals[n]
+        if v.shape[0] != rows:
+            v = v.expand(rows, -1)
+        cols.append(v)
+    return torch.cat(cols, dim=1).contiguous()
+
+
+def _check_discrete(pk: PackedModel, vals: Dict[str, torch.Tensor], nodes: Sequence[str]) -> None:
+    """softmax_nn discrete dims reject values outside the class set (softmax_nn.py:622-625)."""
+    for n in nodes:
+        rec = pk.model.cpds[n]
+        if rec.kind != "softmax_nn" or n not in vals:
+            continue
+        disc = rec.state["_is_discrete"].bool()
+        if not disc.any():
+            continue
+        cv = rec.state["_class_values"].to(vals[n].device)
+        v = vals[n]
+        match = (v.unsqueeze(-1) == cv.unsqueeze(0)).any(-1)
+        if bool(((~match) & disc.to(v.device).unsqueeze(0)).any()):
+            raise ValueError("Found values outside discrete class set.")
+
+
+def _next_seed() -> int:
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+
+# last walk launched (introspection for bench.py's per-kernel timing)
+LAST_LAUNCH: Dict[str, object] = {}
+
+
+def noise_tensor(pk: PackedModel, plan: QueryPlan, noise: Dict[str, Tuple], b: int, n: int) -> torch.Tensor:
+    """Injected draws by node name -> kernel layout [n_latent, 2, b, n, Dmax].
+
+    ``noise[node] = (slot0, slot1)``: slot0 = uniforms of categorical/index choices
+    ([B|1, S] or [B|1, S, D]), slot1 = normals / within-bin uniforms ([B|1, S, D]).
+    """
+    out = torch.zeros(max(len(plan.noise_nodes), 1), 2, b, n, pk.dmax, dtype=torch.float32)
+    for i, node in enumerate(plan.noise_nodes):
+        if node not in noise:
+            continue
+        for slot, v in enumerate(noise[node]):
+            if v is None:
+                continue
+            v = torch.as_tensor(v, dtype=torch.float32).cpu()
+            if v.dim() == 2:
+                v = v.unsqueeze(-1)
+            out[i, slot, :, :, :v.shape[-1]] = v.expand(b, n, v.shape[-1])
+    return out.to(pk.device)
+
+
+def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: int, *,
+             seed: int, offset: int = 0, q_base: int = 0, noise=None,
+             fixed_per_particle: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """One launch of the particle walk; returns (lp [b,n] or empty, x [b,n,n_out_cols])."""
+    n_out_cols = int(plan.out_cols.numel()) if plan.out_nodes else 0
+    noise_b = 1
+    if isinstance(noise, dict):
+        noise = noise_tensor(pk, plan, noise, b, n)
+    if noise is not None:
+        noise = noise.to(device=pk.device, dtype=torch.float32).contiguous()
+        if noise.dim() != 5 or noise.shape[0] < len(plan.noise_nodes) or noise.shape[1] != 2:
+            raise ValueError("noise must be [n_latent, 2, B|1, S, Dmax]")
+        noise_b = int(noise.shape[2])
+        if noise.shape[3] != n or noise.shape[4] != pk.dmax:
+            raise ValueError(f"noise must be [n_latent, 2, B|1, {n}, {pk.dmax}]")
+    LAST_LAUNCH.update(pk=pk, plan=plan, fixed=fixed, b=b, n=n, fixed_per_particle=fixed_per_particle)
+    lp, x = ops.walk(plan.steps, plan.in_cols, pk.params, fixed, noise, plan.out_cols, b, n,
+                     plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
+                     len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
+                     plan.mode != MODE_SAMPLE)
+    if plan.mode != MODE_SAMPLE:
+        lp = lp.view(b, n)
+    if n_out_cols:
+        x = x.view(b, n, n_out_cols)
+    return lp, x
+
+
+class _EngineBase:
+    def __init__(self, n_samples: int = 200, seed: Optional[int] = None, prune_barren: bool = False,
+                 q_base: int = 0, **kwargs):
+        self.n_samples = int(n_samples)
+        self.seed = seed
+        self.prune_barren = bool(prune_barren)
+        self.q_base = int(q_base)
+        self._calls = 0
+
+    def _seed(self, kwargs) -> int:
+        if "seed" in kwargs and kwargs["seed"] is not None:
+            return int(kwargs["seed"])
+        if self.seed is not None:
+            s = int(self.seed) + self._calls
+            self._calls += 1
+            return s
+        return _next_seed()
+
+    @staticmethod
+    def _query(query):
+        ev = dict(getattr(query, "evidence", None) or {})
+        do = dict(getattr(query, "do", None) or {})
+        return query.target, ev, do
+
+
+@register_inference("monte_carlo_marginalization")
+class MonteCarloMarginalization(_EngineBase):
+    """monte_carlo_marginalization.py:12-92 on the GPU."""
+
+    def infer_posterior(self, vbn, query, **kwargs):
+        n = int(kwargs.get("n_samples", self.n_samples))
+        target, ev, do = self._query(query)
+        b = infer_batch_size(ev, do)
+        dev = _device_of(vbn)
+        pk = packed_model(vbn, dev)
+        model = pk.model
+        vals = _fixed_values(query, dev)
+        if target in do:                                                    # Q3
+            return (torch.ones(b, n, device=dev, dtype=torch.float32),
+                    vals[target].unsqueeze(1).expand(b, n, -1))
+        parents = model.parents[target]
+        fixed = [x for x in model.topo if x in vals]
+        _check_discrete(pk, vals, [target] if target in vals else [])
+        prune = self.prune_barren
+        if all(p in vals for p in parents):                                 # Q2 shortcut
+            t_fixed = target in vals
+            nodes = set(parents) | {target}
+            key = ("mcm-short", target, t_fixed)
+            plan = _plan(pk, key, latent=[] if t_fixed else [target],
+                         fixed=[x for x in model.topo if x in nodes and x != target] + ([target] if t_fixed else []),
+                         logp=[target], out_nodes=[target], shared_roots=True, mode=MODE_MCM,
+                         skip=[x for x in model.topo if x not in nodes])
+            b_eff = b if (parents or t_fixed) else 1                        # Q4: root -> (1,S)
+        else:
+            keep = barren_pruned(model, [target]) if prune else set(model.topo)
+            key = ("mcm", target, tuple(sorted(vals)), prune)
+            plan = _plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
+                         fixed=[x for x in fixed if x in keep], logp=[target], out_nodes=[target],
+                         shared_roots=True, mode=MODE_MCM, skip=[x for x in model.topo if x not in keep])
+            b_eff = b
+        fx = _fixed_buffer(plan, vals, b_eff, dev)
+        pdf, xs = run_walk(pk, plan, fx, b_eff, n, seed=self._seed(kwargs), q_base=self.q_base,
+                           noise=kwargs.get("_noise"))
+        return pdf, xs
+
+
+@register_inference("likelihood_weighting")
+class LikelihoodWeighting(_EngineBase):
+    """likelihood_weighting.py:11-82 on the GPU."""
+
+    def __init__(self, n_samples: int = 512, eps: float = 1e-12, normalize: bool = True, **kwargs):
+        super().__init__(n_samples=n_samples, **kwargs)
+        self.eps = float(eps)
+        self.normalize = bool(normalize)
+
+    def _walk(self, vbn, query, n, *, clamp, shared_roots, kwargs, offset=0, noise=None):
+        target, ev, do = self._query(query)
+        b = infer_batch_size(ev, do)
+        dev = _device_of(vbn)
+        pk = packed_model(vbn, dev)
+        model = pk.model
+        vals = _fixed_values(query, dev, clamp=clamp)
+        _check_discrete(pk, vals, list(ev))
+        keep = barren_pruned(model, [target] + list(ev)) if self.prune_barren else set(model.topo)
+        key = ("weighted", target, tuple(sorted(ev)), tuple(sorted(do)), shared_roots, self.prune_barren)
+        plan = _plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
+                     fixed=[x for x in model.topo if x in keep and x in vals],
+                     logp=[x for x in model.topo if x in ev and x in keep], out_nodes=[target],
+                     shared_roots=shared_roots, mode=MODE_WEIGHTED,
+                     skip=[x for x in model.topo if x not in keep])
+        fx = _fixed_buffer(plan, vals, b, dev)
+        seed = kwargs.get("_seed_value")
+        if seed is None:
+            seed = self._seed(kwargs)
+        log_w, xs = run_walk(pk, plan, fx, b, n, seed=seed, offset=offset, q_base=self.q_base, noise=noise)
+        return log_w, xs
+
+    def infer_posterior(self, vbn, query, **kwargs):
+        n = int(kwargs.get("n_samples", self.n_samples))
+        normalize = bool(kwargs.get("normalize", self.normalize))
+        eps = float(kwargs.get("eps", self.eps))
+        log_w, xs = self._walk(vbn, query, n, clamp=True, shared_roots=True, kwargs=kwargs,
+                               offset=int(kwargs.get("_offset", 0)), noise=kwargs.get("_noise"))
+        w, _ = ops.normalize_weights(log_w, normalize, eps)
+        return w, xs
+
+
+@register_inference("importance_sampling")
+class ImportanceSampling(LikelihoodWeighting):
+    """importance_sampling.py:14-93 on the GPU (walk + wave-reduced softmax/ESS + fallback)."""
+
+    def __init__(self, n_samples: int = 200, **kwargs):
+        kwargs.pop("normalize", None)
+        super().__init__(n_samples=n_samples, **kwargs)
+        self.ess_threshold = 0.1
+        self._last_fallback = False
+        self._last_ess: Optional[torch.Tensor] = None
+        self._lw = LikelihoodWeighting(n_samples=self.n_samples, q_base=self.q_base)
+
+    def fallback_needed(self, ess: torch.Tensor, n: int) -> torch.Tensor:
+        """Device-side flag (NaN ESS never triggers; importance_sampling.py:85-86)."""
+        thr = max(1.0, self.ess_threshold * float(n))
+        return (ess < thr).any()
+
+    def infer_posterior(self, vbn, query, **kwargs):
+        n = int(kwargs.get("n_samples", self.n_samples))
+        seed = self._seed(kwargs)
+        log_w, xs = self._walk(vbn, query, n, clamp=False, shared_roots=False,
+                               kwargs={**kwargs, "_seed_value": seed}, noise=kwargs.get("_noise"))
+        w, ess = ops.normalize_weights(log_w, True, 0.0)
+        self._last_ess = ess
+        flag = self.fallback_needed(ess, n)
+        reduce = kwargs.get("_reduce_flag")          # multi-GPU: batch-global decision
+        if reduce is not None:
+            flag = reduce(flag)
+        if bool(flag):                               # host sync, as the reference
+            self._last_fallback = True
+            self._lw.q_base = self.q_base
+            return self._lw.infer_posterior(vbn, query, n_samples=n, _seed_value=seed, _offset=1,
+                                            _noise=kwargs.get("_noise_fallback"))
+        self._last_fallback = False
+        return w, xs
+
+
+@register_sampling("ancestral")
+class AncestralSampler(_EngineBase):
+    """sampling/ancestral.py:57-65 on the GPU."""
+
+    def sample(self, vbn, query, n_samples: Optional[int] = None, **kwargs):
+        n = int(n_samples or self.n_samples)
+        target, ev, do = self._query(query)
+        b = infer_batch_size(ev, do)
+        dev = _device_of(vbn)
+        pk = packed_model(vbn, dev)
+        model = pk.model
+        vals = _fixed_values(query, dev)
+        outs = [target] if target else list(model.topo)
+        keep = barren_pruned(model, outs) if (self.prune_barren and target) else set(model.topo)
+        key = ("ancestral", target, tuple(sorted(vals)), self.prune_barren and bool(target))
+        plan = _plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
+                     fixed=[x for x in model.topo if x in keep and x in vals], logp=[],
+                     out_nodes=outs, shared_roots=True, mode=MODE_SAMPLE,
+                     skip=[x for x in model.topo if x not in keep])
+        fx = _fixed_buffer(plan, vals, b, dev)
+        _, xs = run_walk(pk, plan, fx, b, n, seed=self._seed(kwargs), q_base=self.q_base,
+                         noise=kwargs.get("_noise"))
+        if target:
+            return xs
+        out, c = {}, 0
+        for node in model.topo:
+            d = model.out_dim(node)
+            out[node] = xs[..., c:c + d]
+            c += d
+        return out

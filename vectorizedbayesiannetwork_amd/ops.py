@@ -1,0 +1,123 @@
+"""PyTorch-ROCm custom ops over the C-ABI (``torch.ops.vbn_hip.*``).
+
+* ``vbn_hip::walk``               -> ``vbn_hip_walk``             (particle pass)
+* ``vbn_hip::normalize_weights``  -> ``vbn_hip_normalize_weights`` (softmax over S + ESS)
+
+Both run asynchronously on the current HIP stream, allocate fresh contiguous outputs and
+have fake (meta) implementations for shape inference.  Host-side checks make sure every
+buffer the kernel indexes is large enough before the launch.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import _lib
+from .plan import STEP_INTS
+
+__all__ = ["walk", "normalize_weights"]
+
+
+def _ptr(t: Optional[Tensor]) -> Optional[int]:
+    return None if t is None or t.numel() == 0 else t.data_ptr()
+
+
+def _stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _check_dev(name: str, t: Tensor, dtype: torch.dtype, device: torch.device) -> None:
+    if t.device != device or t.dtype != dtype or not t.is_contiguous():
+        raise ValueError(f"vbn_hip::walk: {name} must be a contiguous {dtype} tensor on {device} "
+                         f"(got {t.dtype} on {t.device}, contiguous={t.is_contiguous()})")
+
+
+@torch.library.custom_op("vbn_hip::walk", mutates_args=())
+def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: Optional[Tensor],
+         out_cols: Tensor, n_queries: int, n_samples: int, n_slots: int, max_out: int,
+         fixed_ld: int, fixed_per_particle: bool, noise_b: int, n_noise: int, dmax: int,
+         n_out_cols: int, mode: int, q_base: int, seed: int, offset: int,
+         want_lp: bool) -> Tuple[Tensor, Tensor]:
+    device = params.device
+    if device.type != "cuda":
+        raise RuntimeError("vbn_hip::walk runs on the GPU only (no CPU fallback); "
+                           f"params are on {device}")
+    _check_dev("steps", steps, torch.int32, device)
+    _check_dev("in_cols", in_cols, torch.int32, device)
+    _check_dev("out_cols", out_cols, torch.int32, device)
+    _check_dev("params", params, torch.float32, device)
+    _check_dev("fixed", fixed, torch.float32, device)
+    if steps.dim() != 2 or steps.shape[1] != STEP_INTS:
+        raise ValueError("vbn_hip::walk: steps must be [n_steps, 32]")
+    total = n_queries * n_samples
+    rows = total if fixed_per_particle else n_queries
+    if fixed.numel() < rows * fixed_ld:
+        raise ValueError(f"vbn_hip::walk: fixed buffer has {fixed.numel()} values, needs {rows}x{fixed_ld}")
+    if noise is not None:
+        _check_dev("noise", noise, torch.float32, device)
+        need = n_noise * 2 * noise_b * n_samples * dmax
+        if noise.numel() < need or noise_b not in (1, n_queries):
+            raise ValueError(f"vbn_hip::walk: noise has {noise.numel()} values, needs {need}")
+    lp = torch.empty(total if want_lp else 0, device=device, dtype=torch.float32)
+    x = torch.empty((total, n_out_cols) if n_out_cols > 0 else (0,), device=device, dtype=torch.float32)
+    a = _lib.VbnWalkArgs()
+    a.steps = _ptr(steps)
+    a.in_cols = _ptr(in_cols)
+    a.params = _ptr(params)
+    a.fixed = _ptr(fixed)
+    a.noise = _ptr(noise)
+    a.out_cols = _ptr(out_cols)
+    a.out_lp = _ptr(lp)
+    a.out_x = _ptr(x)
+    a.n_queries = n_queries
+    a.n_samples = n_samples
+    a.n_steps = steps.shape[0]
+    a.n_slots = n_slots
+    a.max_out = max_out
+    a.fixed_ld = fixed_ld
+    a.fixed_per_particle = int(fixed_per_particle)
+    a.noise_b = noise_b
+    a.dmax = dmax
+    a.n_out_cols = n_out_cols
+    a.mode = mode
+    a.q_base = q_base
+    a.seed = seed & ((1 << 64) - 1)
+    a.offset = offset & ((1 << 64) - 1)
+    lib = _lib.load()
+    with torch.cuda.device(device):
+        _lib.check(lib.vbn_hip_walk(ctypes.byref(a), ctypes.c_void_p(_stream_handle(device))), "vbn_hip_walk")
+    return lp, x
+
+
+@walk.register_fake
+def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
+               fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
+               offset, want_lp):
+    total = n_queries * n_samples
+    lp = params.new_empty(total if want_lp else 0)
+    x = params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))
+    return lp, x
+
+
+@torch.library.custom_op("vbn_hip::normalize_weights", mutates_args=())
+def normalize_weights(log_w: Tensor, normalize: bool, eps: float) -> Tuple[Tensor, Tensor]:
+    if log_w.device.type != "cuda" or log_w.dtype != torch.float32 or log_w.dim() != 2:
+        raise ValueError("vbn_hip::normalize_weights: log_w must be a float32 [B,S] GPU tensor")
+    log_w = log_w.contiguous()
+    b, s = log_w.shape
+    w = torch.empty_like(log_w)
+    ess = torch.empty(b, device=log_w.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(log_w.device):
+        _lib.check(lib.vbn_hip_normalize_weights(
+            _ptr(log_w), _ptr(w), _ptr(ess) if normalize else None, b, s, int(normalize), float(eps),
+            ctypes.c_void_p(_stream_handle(log_w.device))), "vbn_hip_normalize_weights")
+    return w, ess
+
+
+@normalize_weights.register_fake
+def _normalize_fake(log_w, normalize, eps):
+    return torch.empty_like(log_w), log_w.new_empty(log_w.shape[0])

@@ -1,0 +1,393 @@
+"""Plan packer: BNModel + query signature -> device step table, parameter blob, LDS slots.
+
+The reference re-derives its topology per query signature in ``get_inference_state``
+(reference ``vbn/inference/_core.py:57-109``: topo order, parent index tuples, column
+slices, evidence/do masks) and re-reads CPD parameters inside every ATen call.  Here that
+work is split in two device-resident objects:
+
+* :class:`PackedModel` — once per model and device: every CPD's parameters packed into one
+  fp32 blob in the fragment layouts the kernel reads (see ``csrc/vbn_walk.hip``), plus the
+  host-side constants the reference recomputes per call (root loc/scale, mixture weights,
+  KDE kernel scales), computed with the same torch fp32 ops so they are bit-identical.
+* :class:`QueryPlan` — once per (query signature, engine mode): the ``vbn_step`` table
+  (role / flags per node), parent-slot lists and output slots.  Node values live in LDS
+  slots assigned by a liveness scan over the topological order, so a wave's LDS footprint
+  is the peak number of simultaneously live columns, not the total DAG width.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .model import BNModel, CPDRecord
+
+# ---- must match include/vbn_hip.h -------------------------------------------------------
+KIND_ID = {"gaussian_nn": 0, "linear_gaussian": 1, "mdn": 2, "kde": 3, "softmax_nn": 4}
+ROLE_SKIP, ROLE_LATENT, ROLE_FIXED = 0, 1, 2
+F_LOGP, F_ROOT, F_SHARED, F_STANDARDIZE, F_CLIP = 1, 2, 4, 8, 16
+ACT_ID = {"relu": 0, "tanh": 1, "gelu": 2, "elu": 3}
+WITHIN_ID = {"uniform": 0, "triangular": 1, "gaussian": 2}
+MODE_MCM, MODE_WEIGHTED, MODE_SAMPLE = 0, 1, 2
+STEP_INTS = 32
+(S_KIND, S_ROLE, S_FLAGS, S_ACT, S_NIN, S_INOFF, S_OUTCOL, S_OUTDIM, S_FIXEDCOL, S_K, S_NOUT,
+ S_NODEID, S_NOISE, S_AUX0, S_AUX1, S_AUX2, S_OFF_STD, S_OFF_W1, S_OFF_W2, S_OFF_B2, S_OFF_W3,
+ S_OFF_B3, S_OFF_TAIL, S_OFF_PTS) = range(24)
+KDE_CHUNKS = 16
+MLP_HIDDEN = (32, 32)
+KDE_MAX_DIMS = 4
+
+
+def _row(r: int, h: int) -> int:
+    """Row of the 32x32 MFMA accumulator held in register r by lane half h."""
+    return (r & 3) + 8 * (r >> 2) + 4 * h
+
+
+_ROWS = np.array([[_row(r, h) for r in range(16)] for h in range(2)])  # [2,16]
+
+
+class _Blob:
+    def __init__(self):
+        self.parts: List[np.ndarray] = []
+        self.size = 0
+
+    def add(self, arr) -> int:
+        a = np.ascontiguousarray(np.asarray(arr, dtype=np.float32).reshape(-1))
+        off = self.size
+        pad = (-a.size) % 4                      # keep every block 16-byte aligned
+        if pad:
+            a = np.concatenate([a, np.zeros(pad, np.float32)])
+        self.parts.append(a)
+        self.size += a.size
+        return off
+
+    def finish(self) -> np.ndarray:
+        return np.concatenate(self.parts) if self.parts else np.zeros(4, np.float32)
+
+
+def _np(t: torch.Tensor) -> np.ndarray:
+    return t.detach().to("cpu", torch.float32).numpy()
+
+
+def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
+    layers = rec.mlp_layers()
+    hidden = tuple(int(w.shape[0]) for w, _ in layers[:-1])
+    if hidden != MLP_HIDDEN:
+        raise NotImplementedError(
+            f"{rec.kind}: hidden_dims={hidden}; the gfx950 MFMA path implements {MLP_HIDDEN} "
+            "(the reference default, vbn/configs/cpds/*.yaml)")
+    (w1, b1), (w2, b2), (w3, b3) = [(_np(w), _np(b)) for w, b in layers]
+    nin = w1.shape[1]
+    offs: Dict[str, int] = {}
+    if standardize:
+        offs["std"] = blob.add(np.concatenate([_np(rec.state["mean_x"]), _np(rec.state["std_x"])]))
+    else:
+        offs["std"] = 0
+    w1p = np.zeros((2, 16, nin + 1), np.float32)
+    for h in range(2):
+        for s in range(16):
+            w1p[h, s, :nin] = w1[2 * s + h]
+            w1p[h, s, nin] = b1[2 * s + h]
+    offs["w1"] = blob.add(w1p)
+    lane = np.arange(64)
+    w2p = np.zeros((4, 64, 4), np.float32)
+    for q in range(4):
+        for e in range(4):
+            w2p[q, :, e] = w2[lane & 31, 2 * (4 * q + e) + (lane >> 5)]
+    offs["w2"] = blob.add(w2p)
+    offs["b2"] = blob.add(b2[_ROWS])                      # [2,16]
+    offs["w3"] = blob.add(w3[:, _ROWS])                   # [n_out, 2, 16]
+    offs["b3"] = blob.add(b3)
+    offs["n_out"] = w3.shape[0]
+    return offs
+
+
+@dataclass
+class NodePack:
+    kind: int
+    flags: int          # static flags (ROOT, STANDARDIZE, CLIP)
+    act: int
+    n_in: int
+    out_dim: int
+    k: int
+    n_out: int
+    aux0: int
+    aux1: int
+    offs: Dict[str, int]
+
+
+def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
+    kind = rec.kind
+    D = rec.output_dim
+    root = rec.is_root
+    flags = F_ROOT if root else 0
+    act = ACT_ID.get(str(rec.hp("activation") or "relu"), -1)
+    if act < 0:
+        raise ValueError(f"unknown activation {rec.hp('activation')}")
+    st = rec.state
+    offs: Dict[str, int] = {}
+    k = n_out = aux0 = aux1 = 0
+    if kind == "gaussian_nn":
+        if root:
+            loc = st["_loc"].view(1, 1, -1)
+            scale = (F.softplus(st["_log_scale"]) + float(rec.hp("min_scale"))).view(1, 1, -1)
+            std_y = st["std_y"].view(1, 1, -1)
+            loc, scale = loc * std_y + st["mean_y"].view(1, 1, -1), scale * std_y
+            loc, scale = loc.reshape(-1), scale.reshape(-1)
+            offs["tail"] = blob.add(np.concatenate([_np(loc), _np(scale), _np(scale.log())]))
+        else:
+            flags |= F_STANDARDIZE
+            offs.update(_pack_mlp(blob, rec, standardize=True))
+            n_out = offs.pop("n_out")
+            offs["tail"] = blob.add(np.concatenate([_np(st["std_y"]), _np(st["mean_y"]),
+                                                    np.array([rec.hp("min_scale")], np.float32)]))
+    elif kind == "linear_gaussian":
+        var = st["_var"]
+        scale = torch.sqrt(var.clamp(min=float(rec.hp("min_scale")) ** 2))
+        w = st["_weight"]                                  # [n_in, D]
+        offs["tail"] = blob.add(np.concatenate([_np(w.t().contiguous()).reshape(-1), _np(st["_bias"]),
+                                                _np(scale), _np(torch.log(scale))]))
+    elif kind == "mdn":
+        k = int(rec.hp("n_components"))
+        if root:
+            pi = torch.softmax(st["_logits"], dim=-1).clamp_min(1e-5)
+            pi = pi / pi.sum(dim=-1, keepdim=True).clamp_min(1e-12)
+            scale = F.softplus(st["_log_scale"]) + float(rec.hp("min_scale"))
+            log_scale = torch.log(scale)
+            offs["tail"] = blob.add(np.concatenate([
+                _np(pi), _np(torch.log(pi)), _np(st["_loc"]).reshape(-1), _np(scale).reshape(-1),
+                _np(log_scale).reshape(-1), _np(torch.exp(2 * log_scale)).reshape(-1)]))
+        else:
+            offs.update(_pack_mlp(blob, rec, standardize=False))
+            n_out = offs.pop("n_out")
+            if n_out != k * (2 * D) + k:
+                raise ValueError("mdn head width mismatch")
+            offs["tail"] = blob.add(np.array([rec.hp("min_scale")], np.float32))
+    elif kind == "kde":
+        pts_p = rec.extra["parents"].float()
+        pts_y = rec.extra["targets"].float()
+        m = int(pts_y.shape[0])
+        dp = int(pts_p.shape[1]) if pts_p.dim() == 2 else 0
+        if dp > KDE_MAX_DIMS or D > KDE_MAX_DIMS:
+            raise NotImplementedError(f"kde with {dp} parent / {D} target dims (max {KDE_MAX_DIMS})")
+        if m == 0:
+            raise RuntimeError("KDECPD is not fitted yet.")
+        bw = float(rec.hp("bandwidth"))
+        pbw = rec.hp("parent_bandwidth")
+        pbw = bw if pbw is None else float(pbw)
+        min_scale = float(rec.hp("min_scale"))
+        s_p = max(pbw, 1e-3) + min_scale                  # kde.py:106
+        s_y = max(bw, 1e-3) + min_scale
+        noise_scale = max(bw, 1e-3) + min_scale            # kde.py:166,180
+        cy = -0.5 * D * (math.log(2 * math.pi) + 2 * math.log(s_y))
+        offs["tail"] = blob.add(np.array([1.0 / np.float32(s_p), 1.0 / np.float32(s_y),
+                                          noise_scale, cy, math.log(float(m)), 0, 0, 0], np.float32))
+        stride = dp + D
+        stride += (-stride) % 2 if stride > 1 else 0
+        recs = np.zeros((m, stride), np.float32)
+        if dp:
+            recs[:, :dp] = _np(pts_p)
+        recs[:, dp:dp + D] = _np(pts_y)
+        offs["pts"] = blob.add(recs)
+        k, aux0, aux1 = m, dp, stride
+    elif kind == "softmax_nn":
+        if str(rec.hp("mode_when_not_discrete") or "binned") != "binned":
+            raise NotImplementedError("softmax_nn mode_when_not_discrete != 'binned'")
+        if not bool(st["_bins_ready"]):
+            raise RuntimeError("Bins not initialized. Call fit(...) before sampling.")
+        k = int(rec.hp("n_classes"))
+        aux0 = WITHIN_ID[str(rec.hp("within_bin"))]
+        disc = st["_is_discrete"].bool()
+        if D > 31:
+            raise NotImplementedError("softmax_nn with more than 31 output dims")
+        aux1 = int(sum(1 << d for d in range(D) if bool(disc[d])))
+        if bool(rec.hp("within_bin_clip")):
+            flags |= F_CLIP
+        mbw = float(rec.hp("min_bin_width"))
+        offs["tail"] = blob.add(np.concatenate([
+            _np(st["_bin_edges"]).reshape(-1), _np(st["_sample_values"]).reshape(-1),
+            _np(st["_class_values"]).reshape(-1),
+            np.array([rec.hp("within_bin_scale"), mbw, mbw ** 2, 0.0], np.float32)]))
+        if root:
+            if bool(st["_root_ready"]):
+                tab = torch.log_softmax(st["_root_log_probs"].view(D, k) / 1.0, dim=-1)
+            else:
+                tab = st["_logits"].view(D, k) / 1.0
+            offs["pts"] = blob.add(_np(tab))
+        else:
+            offs.update(_pack_mlp(blob, rec, standardize=False))
+            n_out = offs.pop("n_out")
+    else:
+        raise ValueError(kind)
+    return NodePack(kind=KIND_ID[kind], flags=flags, act=max(act, 0), n_in=rec.input_dim,
+                    out_dim=D, k=k, n_out=n_out, aux0=aux0, aux1=aux1, offs=offs)
+
+
+class PackedModel:
+    """Device-resident parameter blob of a :class:`BNModel` (built once per model+device)."""
+
+    def __init__(self, model: BNModel, device: torch.device):
+        self.model = model
+        self.device = torch.device(device)
+        blob = _Blob()
+        blob.add(np.zeros(4, np.float32))                 # offset 0 is never a real block
+        self.nodes: Dict[str, NodePack] = {}
+        for node in model.topo:
+            rec = model.cpds[node]
+            expect = sum(model.out_dim(p) for p in model.parents[node])
+            if rec.input_dim != expect:
+                raise ValueError(f"node {node}: CPD input_dim {rec.input_dim} != parents width {expect}")
+            self.nodes[node] = _pack_node(blob, rec)
+        host = torch.from_numpy(blob.finish())
+        self.params = host.to(self.device)
+        self.node_id = {n: i for i, n in enumerate(model.topo)}
+        self.max_out = max([p.n_out for p in self.nodes.values()] + [1])
+        self.has_kde = any(p.kind == KIND_ID["kde"] for p in self.nodes.values())
+        self.dmax = max(model.out_dim(n) for n in model.topo)
+
+
+@dataclass
+class QueryPlan:
+    steps: torch.Tensor        # int32 [n_steps, 32] (device)
+    in_cols: torch.Tensor      # int32 (device)
+    out_cols: torch.Tensor     # int32 (device)
+    n_steps: int
+    n_slots: int
+    max_out: int
+    fixed_nodes: List[str]     # order of columns in the fixed buffer
+    fixed_ld: int
+    noise_nodes: List[str]     # noise_idx order (latent nodes)
+    out_nodes: List[str]
+    mode: int
+    slot_of: Dict[str, int]
+
+
+def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
+    """Ancestors of ``keep`` (inclusive): every other node is barren for the query."""
+    need = set()
+    stack = list(keep)
+    while stack:
+        n = stack.pop()
+        if n in need:
+            continue
+        need.add(n)
+        stack.extend(model.parents[n])
+    return need
+
+
+def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[str],
+               logp: Sequence[str], out_nodes: Sequence[str], shared_roots: bool, mode: int,
+               skip: Sequence[str] = ()) -> QueryPlan:
+    """Step table for one query signature.
+
+    ``latent``: nodes sampled; ``fixed``: nodes read from the fixed buffer (evidence/do);
+    ``logp``: nodes whose log p(value | parents) is accumulated; ``out_nodes``: nodes whose
+    values are written per particle; ``skip``: nodes not walked at all.
+    """
+    model = packed.model
+    latent_s, fixed_s, logp_s, skip_s = set(latent), set(fixed), set(logp), set(skip)
+    order = [n for n in model.topo if n not in skip_s]
+    for n in order:
+        if (n in latent_s) == (n in fixed_s):
+            raise ValueError(f"node {n} must be exactly one of latent/fixed")
+    # liveness: last step index reading each node's columns
+    pos = {n: i for i, n in enumerate(order)}
+    last = {n: pos[n] for n in order}
+    # a fixed node without log-prob only loads its value: it reads no parents
+    reads = {n: (n in latent_s or n in logp_s) for n in order}
+    for n in order:
+        if not reads[n]:
+            continue
+        for p in model.parents[n]:
+            if p not in pos:
+                raise ValueError(f"node {n} needs skipped parent {p}")
+            last[p] = max(last[p], pos[n])
+    for n in out_nodes:
+        last[n] = len(order) + 1
+    free: List[int] = []
+    n_slots = 0
+    slot_of: Dict[str, int] = {}
+    release: Dict[int, List[str]] = {}
+    for i, n in enumerate(order):
+        d = model.out_dim(n)
+        # contiguous run of d slots: take from the free list if a run exists
+        base = None
+        if d == 1 and free:
+            free.sort()
+            base = free.pop(0)
+        elif d > 1:
+            fs = sorted(free)
+            for j in range(len(fs) - d + 1):
+                if fs[j + d - 1] - fs[j] == d - 1:
+                    base = fs[j]
+                    for q in range(d):
+                        free.remove(base + q)
+                    break
+        if base is None:
+            base = n_slots
+            n_slots += d
+        slot_of[n] = base
+        release.setdefault(last[n], []).append(n)
+        for m in release.pop(i, []):
+            if m != n or last[n] == i:
+                free.extend(range(slot_of[m], slot_of[m] + model.out_dim(m)))
+    fixed_nodes = [n for n in order if n in fixed_s]
+    fixed_col = {}
+    c = 0
+    for n in fixed_nodes:
+        fixed_col[n] = c
+        c += model.out_dim(n)
+    noise_nodes = [n for n in order if n in latent_s]
+    noise_idx = {n: i for i, n in enumerate(noise_nodes)}
+    steps = np.zeros((len(order), STEP_INTS), np.int32)
+    in_cols: List[int] = []
+    for i, n in enumerate(order):
+        npk = packed.nodes[n]
+        row = steps[i]
+        row[S_KIND] = npk.kind
+        row[S_ROLE] = ROLE_LATENT if n in latent_s else ROLE_FIXED
+        fl = npk.flags
+        if n in logp_s:
+            fl |= F_LOGP
+        if shared_roots and (npk.flags & F_ROOT):
+            fl |= F_SHARED
+        row[S_FLAGS] = fl
+        row[S_ACT] = npk.act
+        row[S_NIN] = npk.n_in
+        row[S_INOFF] = len(in_cols)
+        if reads[n]:
+            for p in model.parents[n]:
+                in_cols.extend(range(slot_of[p], slot_of[p] + model.out_dim(p)))
+        row[S_OUTCOL] = slot_of[n]
+        row[S_OUTDIM] = npk.out_dim
+        row[S_FIXEDCOL] = fixed_col.get(n, 0)
+        row[S_K] = npk.k
+        row[S_NOUT] = npk.n_out
+        row[S_NODEID] = packed.node_id[n]
+        row[S_NOISE] = noise_idx.get(n, 0)
+        row[S_AUX0] = npk.aux0
+        row[S_AUX1] = npk.aux1
+        for key, idx in (("std", S_OFF_STD), ("w1", S_OFF_W1), ("w2", S_OFF_W2), ("b2", S_OFF_B2),
+                         ("w3", S_OFF_W3), ("b3", S_OFF_B3), ("tail", S_OFF_TAIL), ("pts", S_OFF_PTS)):
+            row[idx] = npk.offs.get(key, 0)
+    out_cols: List[int] = []
+    for n in out_nodes:
+        out_cols.extend(range(slot_of[n], slot_of[n] + model.out_dim(n)))
+    dev = packed.device
+
+    def t(a):
+        a = np.asarray(a, np.int32).reshape(-1) if len(a) else np.zeros(1, np.int32)
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+    max_out = max([packed.nodes[n].n_out for n in order] + [1])
+    if any(packed.nodes[n].kind == KIND_ID["kde"] for n in order):
+        max_out = max(max_out, KDE_CHUNKS)
+    return QueryPlan(
+        steps=torch.from_numpy(steps).to(dev) if len(order) else torch.zeros(1, STEP_INTS, dtype=torch.int32, device=dev),
+        in_cols=t(in_cols), out_cols=t(out_cols), n_steps=len(order), n_slots=max(n_slots, 1),
+        max_out=max_out, fixed_nodes=fixed_nodes, fixed_ld=max(c, 1), noise_nodes=noise_nodes,
+        out_nodes=list(out_nodes), mode=mode, slot_of=slot_of)
