@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 1
+#define VBN_ABI_VERSION 2
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001
@@ -105,6 +105,7 @@ typedef struct vbn_walk_args {
   int32_t dmax;
   int32_t n_out_cols;
   int32_t mode;            /* enum vbn_mode                                        */
+  int32_t kind_mask;       /* CPD kinds walked: 1<<kind, | 32 if a non-relu activation */
   int64_t q_base;          /* global index of query 0 (multi-GPU shards)            */
   uint64_t seed;
   uint64_t offset;         /* RNG stream offset (one per engine call)               */

@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -47,6 +47,7 @@ class VbnWalkArgs(ctypes.Structure):
         ("dmax", ctypes.c_int32),
         ("n_out_cols", ctypes.c_int32),
         ("mode", ctypes.c_int32),
+        ("kind_mask", ctypes.c_int32),
         ("q_base", ctypes.c_int64),
         ("seed", ctypes.c_uint64),
         ("offset", ctypes.c_uint64),

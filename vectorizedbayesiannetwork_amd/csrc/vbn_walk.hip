@@ -47,7 +47,10 @@ __device__ __forceinline__ void wave_sync() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-__device__ __forceinline__ float relu_nan(float x) { return x < 0.f ? 0.f : x; }  // torch.relu keeps NaN
+// relu as one v_max_i32 on the float's bits (negative floats are negative ints; -0 -> +0).
+// fmaxf would add a canonicalising v_max(x, x) in IEEE mode, inline asm would hide the
+// MFMA->VALU read hazard from the compiler.  NaN parents are handled by the caller.
+__device__ __forceinline__ float relu_nan(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
 template <int ACT>
 __device__ __forceinline__ float act_fn(float x) {
@@ -89,6 +92,8 @@ struct Draw {
 };
 
 struct Lane {
+  const float* P;        // parameter blob (from a __restrict__ kernel argument)
+  const int32_t* ic;     // parent column slots (from a __restrict__ kernel argument)
   float* vals;   // LDS [n_slots][64]
   float* scr;    // LDS [max_out][64]
   int lane;
@@ -133,113 +138,146 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
 // ------------------------------------------------------------------------------------------
 // MLP (in -> 32 -> 32 -> n_out) for the wave's 64 particles; head outputs to scr[j][lane].
 //
+// Two 32-particle groups per wave (g = 0: particles 0-31, g = 1: 32-63).  Both hidden layers
+// run on v_mfma_f32_32x32x2_f32 with the hidden unit on M and the particle on N; biases are
+// folded in as an extra K column fed a constant 1, so no accumulator is ever initialised.
+//   layer 1: K = n_in + 1 (z, 1),  A = W1aug fragments, B = z of the lane's particle
+//   layer 2: K = 32 + 1 (h1, 1),   the layer-1 accumulator IS the B operand: register s of
+//            lane half h holds hidden row(s, h), so k-step s pairs rows (row(s,0), row(s,1))
+//            and the host packs W2 columns in that order.
+//   head   : 16 v_permlane32_swap transpose the layer-2 accumulators so lane l holds all 32
+//            hidden units of particle l; the head then runs on VALU with wave-uniform weights.
+//
 // Parameter blocks (packed by vectorizedbayesiannetwork_amd/plan.py):
-//   off_std : mean_x[n_in], std_x[n_in]                          (gaussian_nn only)
-//   off_w1  : [half 2][s 16][n_in + 1]  = W1[2s+half][:], b1[2s+half]
-//   off_w2  : [q 4][lane 64][4]        = W2[lane&31][2(4q+e)+(lane>>5)]   (A fragments)
-//   off_b2  : [half 2][r 16]           = b2[row(r, half)]
-//   off_w3  : [j][half 2][r 16]        = W3[j][row(r, half)]
+//   off_std : mean_x[n_in], 1/std_x[n_in]                            (gaussian_nn only)
+//   off_w1  : [t][64]  lane l: W1aug[l&31][2t + (l>>5)],  W1aug = [W1 | b1 | 0]
+//   off_w2  : [q 5][lane 64][4], step s = 4q+e: s<16: W2[l&31][row(s, l>>5)];
+//             s = 16: (l>>5) == 0 ? b2[l&31] : 0;  s > 16: 0
+//   off_w3  : [n_out][32] = W3[j][row(r,0)] (r<16) ++ W3[j][row(r,1)]
 //   off_b3  : [n_out]
-// with row(r, h) = (r&3) + 8(r>>2) + 4h, the 32x32 MFMA accumulator row of register r.
+// with row(r, h) = (r&3) + 8(r>>2) + 4h, the 32x32 accumulator row of register r, half h.
 // ------------------------------------------------------------------------------------------
 
-template <int ACT, bool STD>
+// layer-1 B operand of k-step t for group g: z[2t + half] of particle (c + 32 g); the
+// bias column n_in is the constant 1, columns beyond it are 0.
+template <bool STD, int NIN>
+__device__ __forceinline__ float l1_operand(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
+                                            int t, int g) {
+  const float* __restrict__ P = L.P;
+  const int half = L.lane >> 5;
+  const int nin = NIN > 0 ? NIN : st.n_in;
+  const int kk = 2 * t + half;
+  const int ke = min(2 * t, nin - 1), ko = min(2 * t + 1, nin - 1);
+  const int slot = half ? L.ic[st.in_off + ko] : L.ic[st.in_off + ke];
+  float z = L.vals[slot * WAVE + (L.lane & 31) + 32 * g];
+  if (STD) {
+    const float m = half ? P[st.off_std + ko] : P[st.off_std + ke];
+    const float is = half ? P[st.off_std + nin + ko] : P[st.off_std + nin + ke];
+    z = (z - m) * is;
+  }
+  return kk < nin ? z : (kk == nin ? 1.0f : 0.0f);
+}
+
+template <int ACT, bool STD, int NIN>
 __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
-  const float* __restrict__ P = A.params;
+  const float* __restrict__ P = L.P;
   const int lane = L.lane;
   const int half = lane >> 5;
-  const int c = lane & 31;
-  const int nin = st.n_in;
+  const int nin = NIN > 0 ? NIN : st.n_in;
+  const int t1 = (nin + 2) >> 1;                  // layer-1 k-steps incl. the bias column
 
-  float h1a[16], h1b[16];
-  const float* w1 = P + st.off_w1 + half * 16 * (nin + 1);
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const float bias = w1[s * (nin + 1) + nin];
-    h1a[s] = bias;
-    h1b[s] = bias;
-  }
+  bool nan_in = false;                            // torch keeps NaN through Linear/act
   for (int d = 0; d < nin; ++d) {
-    const int slot = A.in_cols[st.in_off + d];
-    float za = L.vals[slot * WAVE + c];
-    float zb = L.vals[slot * WAVE + 32 + c];
-    if (STD) {
-      const float m = P[st.off_std + d];
-      const float sd = P[st.off_std + nin + d];
-      za = (za - m) / sd;
-      zb = (zb - m) / sd;
-    }
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const float w = w1[s * (nin + 1) + d];
-      h1a[s] = fmaf(w, za, h1a[s]);
-      h1b[s] = fmaf(w, zb, h1b[s]);
-    }
+    const float v = L.vals[L.ic[st.in_off + d] * WAVE + lane];
+    nan_in |= (v != v);
   }
 
-  float w2[16];
   const float4* w2p = reinterpret_cast<const float4*>(P + st.off_w2);
+  float w2[20];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < 5; ++q) {
     const float4 v = w2p[q * WAVE + lane];
     w2[4 * q + 0] = v.x;
     w2[4 * q + 1] = v.y;
     w2[4 * q + 2] = v.z;
     w2[4 * q + 3] = v.w;
   }
-  f32x16 acc0, acc1;
-  const float* b2 = P + st.off_b2 + half * 16;
+  const float one = half ? 0.f : 1.f;
+
+  f32x16 h2[2];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    acc0[r] = b2[r];
-    acc1[r] = b2[r];
-  }
+  for (int g = 0; g < 2; ++g) {
+    // layer 1 (+ bias column)
+    f32x16 a = {};
+    if (NIN > 0) {
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[s], act_fn<ACT>(h1a[s]), acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[s], act_fn<ACT>(h1b[s]), acc1, 0, 0, 0);
-  }
+      for (int t = 0; t < (NIN + 2) / 2; ++t)
+        a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
+                                                 l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
+    } else {
+      for (int t = 0; t < t1; ++t)
+        a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
+                                                 l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
+    }
+    // layer 2 (+ bias step 16): the layer-1 accumulator is the B operand
+    f32x16 b = {};
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    acc0[r] = act_fn<ACT>(acc0[r]);
-    acc1[r] = act_fn<ACT>(acc1[r]);
+    for (int s2 = 0; s2 < 16; ++s2)
+      b = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[s2], act_fn<ACT>(a[s2]), b, 0, 0, 0);
+    h2[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[16], one, b, 0, 0, 0);
   }
 
-  const int nout = st.n_out;
-  for (int j = 0; j < nout; ++j) {
-    const float4* w3 = reinterpret_cast<const float4*>(P + st.off_w3 + (j * 2 + half) * 16);
-    float p0 = 0.f, p1 = 0.f;
+  // transpose: lane l <- all 32 hidden units of particle l
+  float X[16], Y[16];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 w = w3[q];
-      p0 = fmaf(w.x, acc0[4 * q + 0], p0);
-      p1 = fmaf(w.x, acc1[4 * q + 0], p1);
-      p0 = fmaf(w.y, acc0[4 * q + 1], p0);
-      p1 = fmaf(w.y, acc1[4 * q + 1], p1);
-      p0 = fmaf(w.z, acc0[4 * q + 2], p0);
-      p1 = fmaf(w.z, acc1[4 * q + 2], p1);
-      p0 = fmaf(w.w, acc0[4 * q + 3], p0);
-      p1 = fmaf(w.w, acc1[4 * q + 3], p1);
-    }
-    // lanes 0-31 take group 0's two halves, lanes 32-63 group 1's: one swap.
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0), __float_as_uint(p1), false, false);
-    const float out = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-    L.scr[j * WAVE + lane] = out + P[st.off_b3 + j];
+  for (int r = 0; r < 16; ++r) {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(h2[0][r]), __float_as_uint(h2[1][r]), false, false);
+    X[r] = act_fn<ACT>(__uint_as_float(sw[0]));   // hidden row(r, 0)
+    Y[r] = act_fn<ACT>(__uint_as_float(sw[1]));   // hidden row(r, 1)
+  }
+
+  // head (wave-uniform weights)
+  const int nout = st.n_out;
+  const float* __restrict__ w3 = P + st.off_w3;
+#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+  for (int j = 0; j < nout; ++j) {
+    float o = P[st.off_b3 + j];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o = fmaf(w3[j * 32 + r], X[r], o);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o = fmaf(w3[j * 32 + 16 + r], Y[r], o);
+    L.scr[j * WAVE + lane] = nan_in ? __int_as_float(0x7fc00000) : o;
   }
   wave_sync();
 }
 
+template <int ACT, bool STD>
+__device__ __forceinline__ void mlp_nin(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  switch (st.n_in) {
+    case 1: mlp_forward<ACT, STD, 1>(A, st, L); break;
+    case 2: mlp_forward<ACT, STD, 2>(A, st, L); break;
+    case 3: mlp_forward<ACT, STD, 3>(A, st, L); break;
+    default: mlp_forward<ACT, STD, 0>(A, st, L); break;
+  }
+}
+
+// KM bit 5: some NN CPD uses a non-relu activation
+template <unsigned KM>
 __device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
   const bool sd = (st.flags & VBN_F_STANDARDIZE) != 0;
-  switch (st.act * 2 + (sd ? 1 : 0)) {
-    case 0: mlp_forward<VBN_ACT_RELU, false>(A, st, L); break;
-    case 1: mlp_forward<VBN_ACT_RELU, true>(A, st, L); break;
-    case 2: mlp_forward<VBN_ACT_TANH, false>(A, st, L); break;
-    case 3: mlp_forward<VBN_ACT_TANH, true>(A, st, L); break;
-    case 4: mlp_forward<VBN_ACT_GELU, false>(A, st, L); break;
-    case 5: mlp_forward<VBN_ACT_GELU, true>(A, st, L); break;
-    case 6: mlp_forward<VBN_ACT_ELU, false>(A, st, L); break;
-    default: mlp_forward<VBN_ACT_ELU, true>(A, st, L); break;
+  if (!(KM & 32) || st.act == VBN_ACT_RELU) {
+    if (sd) mlp_nin<VBN_ACT_RELU, true>(A, st, L); else mlp_nin<VBN_ACT_RELU, false>(A, st, L);
+    return;
+  }
+  if constexpr ((KM & 32) != 0) {
+    switch (st.act * 2 + (sd ? 1 : 0)) {
+      case 2: mlp_nin<VBN_ACT_TANH, false>(A, st, L); break;
+      case 3: mlp_nin<VBN_ACT_TANH, true>(A, st, L); break;
+      case 4: mlp_nin<VBN_ACT_GELU, false>(A, st, L); break;
+      case 5: mlp_nin<VBN_ACT_GELU, true>(A, st, L); break;
+      case 6: mlp_nin<VBN_ACT_ELU, false>(A, st, L); break;
+      default: mlp_nin<VBN_ACT_ELU, true>(A, st, L); break;
+    }
   }
 }
 
@@ -251,9 +289,10 @@ __device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& 
 //   tail (non-root): std_y[D], mean_y[D], min_scale
 //   tail (root)    : loc[D], scale[D], log_scale[D]
 // ------------------------------------------------------------------------------------------
+template <unsigned KM>
 __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
 #pragma clang fp contract(off)
-  const float* __restrict__ P = A.params;
+  const float* __restrict__ P = L.P;
   const int D = st.out_dim;
   const bool latent = st.role == VBN_ROLE_LATENT;
   const bool want_lp = (st.flags & VBN_F_LOGP) != 0;
@@ -277,7 +316,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
     }
     return;
   }
-  run_mlp(A, st, L);
+  run_mlp<KM>(A, st, L);
   const float min_scale = t[2 * D];
   float acc = 0.f;
   for (int d = 0; d < D; ++d) {
@@ -308,7 +347,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ void step_linear_gaussian(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
 #pragma clang fp contract(off)
-  const float* __restrict__ P = A.params;
+  const float* __restrict__ P = L.P;
   const int D = st.out_dim, nin = st.n_in;
   const float* t = P + st.off_tail;
   const float* W = t;
@@ -319,7 +358,7 @@ __device__ __forceinline__ void step_linear_gaussian(const vbn_walk_args& A, con
   float acc = 0.f;
   for (int d = 0; d < D; ++d) {
     float mu = 0.f;
-    for (int i = 0; i < nin; ++i) mu = fmaf(vread(L, A.in_cols[st.in_off + i]), W[d * nin + i], mu);
+    for (int i = 0; i < nin; ++i) mu = fmaf(vread(L, L.ic[st.in_off + i]), W[d * nin + i], mu);
     const float loc = (nin > 0) ? mu + bias[d] : bias[d];
     float x;
     if (latent) {
@@ -359,9 +398,10 @@ __device__ __forceinline__ int inv_cdf(int K, float u, F prob) {
 //   non-root: scr = [logits K][comp k: loc D, raw_scale D];  tail: min_scale
 //   root    : tail = pi[K], log_pi[K], loc[K*D], scale[K*D], log_scale[K*D], var[K*D]
 // ------------------------------------------------------------------------------------------
+template <unsigned KM>
 __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
 #pragma clang fp contract(off)
-  const float* __restrict__ P = A.params;
+  const float* __restrict__ P = L.P;
   const int D = st.out_dim, K = st.k;
   const float* t = P + st.off_tail;
   const bool root = (st.flags & VBN_F_ROOT) != 0;
@@ -371,7 +411,7 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
   float* scr = L.scr;
   float min_scale = 0.f, lmax = 0.f, lsum = 1.f, psum = 1.f;
   if (!root) {
-    run_mlp(A, st, L);
+    run_mlp<KM>(A, st, L);
     min_scale = t[0];
     // pi = softmax(logits).clamp_min(1e-5); pi /= sum (mdn.py:227-228)
     lmax = -INFINITY;
@@ -441,9 +481,10 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
 //   tail: edges[D][C+1], sample_values[D][C], class_values[D][C], within_scale, min_bw, min_bw2
 //   aux0 = within-bin mode, aux1 = discrete-dim bit mask
 // ------------------------------------------------------------------------------------------
+template <unsigned KM>
 __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
 #pragma clang fp contract(off)
-  const float* __restrict__ P = A.params;
+  const float* __restrict__ P = L.P;
   const int D = st.out_dim, C = st.k;
   const float* t = P + st.off_tail;
   const float* edges = t;
@@ -457,7 +498,7 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
   const bool clip = (st.flags & VBN_F_CLIP) != 0;
   const int mode = st.aux0;
   const int lane = L.lane;
-  if (!root) run_mlp(A, st, L);
+  if (!root) run_mlp<KM>(A, st, L);
   float lp_acc = 0.f;
   for (int d = 0; d < D; ++d) {
     auto logit = [&](int c) -> float {
@@ -562,7 +603,7 @@ __device__ __forceinline__ float kde_qp(const float* __restrict__ pt, const floa
     }
   } else {
     for (int i = 0; i < dp; ++i) {
-      const float df = (vread(L, A.in_cols[st.in_off + i]) - pt[i]) * inv;
+      const float df = (vread(L, L.ic[st.in_off + i]) - pt[i]) * inv;
       q = fmaf(df, df, q);
     }
   }
@@ -587,7 +628,7 @@ __device__ __forceinline__ float kde_qy(const float* __restrict__ pty, float x0,
 template <int DP, int DY>
 __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
 #pragma clang fp contract(off)
-  const float* __restrict__ P = A.params;
+  const float* __restrict__ P = L.P;
   const float* __restrict__ pts = P + st.off_pts;
   const int M = st.k, dp = DP >= 0 ? DP : st.aux0, stride = st.aux1, D = DY > 0 ? DY : st.out_dim;
   const float* t = P + st.off_tail;
@@ -596,7 +637,7 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
   const int lane = L.lane;
   float pv[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < (DP > 0 ? DP : 0); ++i) pv[i] = vread(L, A.in_cols[st.in_off + i]);
+  for (int i = 0; i < (DP > 0 ? DP : 0); ++i) pv[i] = vread(L, L.ic[st.in_off + i]);
 
   if (st.role == VBN_ROLE_LATENT) {
     const Draw r0 = get_draw(A, st, 0, L);
@@ -721,9 +762,17 @@ __device__ __forceinline__ void step_kde(const vbn_walk_args& A, const vbn_step&
 // ------------------------------------------------------------------------------------------
 // the walk
 // ------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(WAVE) vbn_walk_kernel(const vbn_walk_args A) {
+// KM: bit0 gaussian_nn, bit1 linear_gaussian, bit2 mdn, bit3 kde, bit4 softmax_nn,
+// bit5 non-relu activations.  Each instantiation only carries the code (and registers) of
+// the CPD kinds a plan uses.
+template <unsigned KM>
+__global__ void __launch_bounds__(WAVE) vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params,
+                                                        const vbn_step* __restrict__ steps,
+                                                        const int32_t* __restrict__ in_cols) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   Lane L;
+  L.P = params;
+  L.ic = in_cols;
   L.lane = threadIdx.x;
   L.vals = smem;
   L.scr = smem + A.n_slots * WAVE;
@@ -736,7 +785,7 @@ __global__ void __launch_bounds__(WAVE) vbn_walk_kernel(const vbn_walk_args A) {
 
   float lp = 0.f;
   for (int i = 0; i < A.n_steps; ++i) {
-    const vbn_step st = A.steps[i];
+    const vbn_step st = steps[i];
     if (st.role == VBN_ROLE_SKIP) continue;
     if (st.role == VBN_ROLE_FIXED && !(st.flags & VBN_F_LOGP)) {   // evidence / do: value only
       for (int d = 0; d < st.out_dim; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
@@ -744,11 +793,11 @@ __global__ void __launch_bounds__(WAVE) vbn_walk_kernel(const vbn_walk_args A) {
       continue;
     }
     switch (st.kind) {
-      case VBN_KIND_GAUSSIAN_NN: step_gaussian_nn(A, st, L, lp); break;
-      case VBN_KIND_LINEAR_GAUSSIAN: step_linear_gaussian(A, st, L, lp); break;
-      case VBN_KIND_MDN: step_mdn(A, st, L, lp); break;
-      case VBN_KIND_KDE: step_kde(A, st, L, lp); break;
-      default: step_softmax_nn(A, st, L, lp); break;
+      case VBN_KIND_GAUSSIAN_NN: if constexpr ((KM & 1) != 0) step_gaussian_nn<KM>(A, st, L, lp); break;
+      case VBN_KIND_LINEAR_GAUSSIAN: if constexpr ((KM & 2) != 0) step_linear_gaussian(A, st, L, lp); break;
+      case VBN_KIND_MDN: if constexpr ((KM & 4) != 0) step_mdn<KM>(A, st, L, lp); break;
+      case VBN_KIND_KDE: if constexpr ((KM & 8) != 0) step_kde(A, st, L, lp); break;
+      default: if constexpr ((KM & 16) != 0) step_softmax_nn<KM>(A, st, L, lp); break;
     }
     wave_sync();
   }
@@ -860,8 +909,27 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   const int64_t total = a->n_queries * (int64_t)a->n_samples;
   const int64_t blocks = (total + WAVE - 1) / WAVE;
   if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
-  hipLaunchKernelGGL(vbn_walk_kernel, dim3((unsigned)blocks), dim3(WAVE), (size_t)lds,
-                     (hipStream_t)stream, *a);
+  // smallest instantiated kind set covering the plan
+  static const unsigned masks[] = {1u, 2u, 3u, 4u, 8u, 16u, 20u, 23u, 31u, 63u};
+  const unsigned want = (unsigned)a->kind_mask & 63u;
+  unsigned km = 63u;
+  for (unsigned m : masks) {
+    if ((m & want) == want && __builtin_popcount(m) < __builtin_popcount(km)) km = m;
+  }
+  const dim3 grid((unsigned)blocks), block(WAVE);
+  hipStream_t st = (hipStream_t)stream;
+  switch (km) {
+    case 1u: hipLaunchKernelGGL(vbn_walk_kernel<1u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+    case 2u: hipLaunchKernelGGL(vbn_walk_kernel<2u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+    case 3u: hipLaunchKernelGGL(vbn_walk_kernel<3u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+    case 4u: hipLaunchKernelGGL(vbn_walk_kernel<4u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+    case 8u: hipLaunchKernelGGL(vbn_walk_kernel<8u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+    case 16u: hipLaunchKernelGGL(vbn_walk_kernel<16u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+    case 20u: hipLaunchKernelGGL(vbn_walk_kernel<20u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+    case 23u: hipLaunchKernelGGL(vbn_walk_kernel<23u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+    case 31u: hipLaunchKernelGGL(vbn_walk_kernel<31u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+    default: hipLaunchKernelGGL(vbn_walk_kernel<63u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;

@@ -195,7 +195,7 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
     lp, x = ops.walk(plan.steps, plan.in_cols, pk.params, fixed, noise, plan.out_cols, b, n,
                      plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
                      len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
-                     plan.mode != MODE_SAMPLE)
+                     plan.mode != MODE_SAMPLE, plan.kind_mask)
     if plan.mode != MODE_SAMPLE:
         lp = lp.view(b, n)
     if n_out_cols:

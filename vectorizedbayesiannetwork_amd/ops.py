@@ -40,7 +40,7 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
          out_cols: Tensor, n_queries: int, n_samples: int, n_slots: int, max_out: int,
          fixed_ld: int, fixed_per_particle: bool, noise_b: int, n_noise: int, dmax: int,
          n_out_cols: int, mode: int, q_base: int, seed: int, offset: int,
-         want_lp: bool) -> Tuple[Tensor, Tensor]:
+         want_lp: bool, kind_mask: int = 63) -> Tuple[Tensor, Tensor]:
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::walk runs on the GPU only (no CPU fallback); "
@@ -83,6 +83,7 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
     a.dmax = dmax
     a.n_out_cols = n_out_cols
     a.mode = mode
+    a.kind_mask = kind_mask
     a.q_base = q_base
     a.seed = seed & ((1 << 64) - 1)
     a.offset = offset & ((1 << 64) - 1)
@@ -95,7 +96,7 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
 @walk.register_fake
 def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
-               offset, want_lp):
+               offset, want_lp, kind_mask=63):
     total = n_queries * n_samples
     lp = params.new_empty(total if want_lp else 0)
     x = params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))

@@ -74,6 +74,7 @@ def _np(t: torch.Tensor) -> np.ndarray:
 
 
 def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
+    """MFMA fragment layouts of csrc/vbn_walk.hip mlp_forward (biases as constant-1 K columns)."""
     layers = rec.mlp_layers()
     hidden = tuple(int(w.shape[0]) for w, _ in layers[:-1])
     if hidden != MLP_HIDDEN:
@@ -84,23 +85,23 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     nin = w1.shape[1]
     offs: Dict[str, int] = {}
     if standardize:
-        offs["std"] = blob.add(np.concatenate([_np(rec.state["mean_x"]), _np(rec.state["std_x"])]))
+        inv = (np.float32(1.0) / _np(rec.state["std_x"]).astype(np.float32)).astype(np.float32)
+        offs["std"] = blob.add(np.concatenate([_np(rec.state["mean_x"]), inv]))
     else:
         offs["std"] = 0
-    w1p = np.zeros((2, 16, nin + 1), np.float32)
-    for h in range(2):
-        for s in range(16):
-            w1p[h, s, :nin] = w1[2 * s + h]
-            w1p[h, s, nin] = b1[2 * s + h]
-    offs["w1"] = blob.add(w1p)
+    t1 = (nin + 2) // 2
+    w1aug = np.zeros((32, 2 * t1), np.float32)
+    w1aug[:, :nin] = w1
+    w1aug[:, nin] = b1
     lane = np.arange(64)
-    w2p = np.zeros((4, 64, 4), np.float32)
-    for q in range(4):
-        for e in range(4):
-            w2p[q, :, e] = w2[lane & 31, 2 * (4 * q + e) + (lane >> 5)]
-    offs["w2"] = blob.add(w2p)
-    offs["b2"] = blob.add(b2[_ROWS])                      # [2,16]
-    offs["w3"] = blob.add(w3[:, _ROWS])                   # [n_out, 2, 16]
+    w1f = np.stack([w1aug[lane & 31, 2 * t + (lane >> 5)] for t in range(t1)])   # [t1, 64]
+    offs["w1"] = blob.add(w1f)
+    w2f = np.zeros((20, 64), np.float32)
+    for s in range(16):
+        w2f[s] = w2[lane & 31, _ROWS[lane >> 5, s]]
+    w2f[16] = np.where(lane < 32, b2[lane & 31], 0.0)
+    offs["w2"] = blob.add(w2f.reshape(5, 4, 64).transpose(0, 2, 1))            # [5, 64, 4]
+    offs["w3"] = blob.add(np.concatenate([w3[:, _ROWS[0]], w3[:, _ROWS[1]]], axis=1))  # [n_out, 32]
     offs["b3"] = blob.add(b3)
     offs["n_out"] = w3.shape[0]
     return offs
@@ -264,6 +265,7 @@ class QueryPlan:
     out_nodes: List[str]
     mode: int
     slot_of: Dict[str, int]
+    kind_mask: int = 63       # CPD kinds the walk evaluates (selects the kernel instantiation)
 
 
 def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
@@ -383,6 +385,13 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         a = np.asarray(a, np.int32).reshape(-1) if len(a) else np.zeros(1, np.int32)
         return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
+    kind_mask = 0
+    for n in order:
+        if n in latent_s or n in logp_s:
+            npk = packed.nodes[n]
+            kind_mask |= 1 << npk.kind
+            if npk.n_out and npk.act != ACT_ID["relu"]:
+                kind_mask |= 32
     max_out = max([packed.nodes[n].n_out for n in order] + [1])
     if any(packed.nodes[n].kind == KIND_ID["kde"] for n in order):
         max_out = max(max_out, KDE_CHUNKS)
@@ -390,4 +399,4 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         steps=torch.from_numpy(steps).to(dev) if len(order) else torch.zeros(1, STEP_INTS, dtype=torch.int32, device=dev),
         in_cols=t(in_cols), out_cols=t(out_cols), n_steps=len(order), n_slots=max(n_slots, 1),
         max_out=max_out, fixed_nodes=fixed_nodes, fixed_ld=max(c, 1), noise_nodes=noise_nodes,
-        out_nodes=list(out_nodes), mode=mode, slot_of=slot_of)
+        out_nodes=list(out_nodes), mode=mode, slot_of=slot_of, kind_mask=kind_mask)
