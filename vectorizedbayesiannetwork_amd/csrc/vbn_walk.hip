@@ -60,16 +60,25 @@ __device__ __forceinline__ float act_fn(float x) {
   return x > 0.f ? x : expm1f(x);  // ELU(alpha=1)
 }
 
-// F.softplus(beta=1, threshold=20) (reference cpds/utils.py:6-7)
-__device__ __forceinline__ float softplus_t(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+// F.softplus(beta=1, threshold=20) (reference cpds/utils.py:6-7) with hardware exp/log:
+// log1p(e) as Kahan's log(u) * e / (u - 1) (u - 1 is exact) for x >= -5, a 4-term series
+// below (relative error < 1e-9 there).
+__device__ __forceinline__ float softplus_t(float x) {
+  if (x > 20.f) return x;
+  const float e = __expf(x);
+  if (x < -5.f) return e * (1.f - e * (0.5f - e * (0.33333334f - e * 0.25f)));
+  const float u = 1.0f + e;
+  return __logf(u) * __fdividef(e, u - 1.0f);
+}
 
 // Philox-4x32-10 counter-based RNG.
 __device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;   // one v_mad_u64_u32 per product
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k.x, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k.y,
+                   (uint32_t)p0);
     k.x += 0x9E3779B9u;
     k.y += 0xBB67AE85u;
   }
@@ -139,20 +148,20 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
 // MLP (in -> 32 -> 32 -> n_out) for the wave's 64 particles; head outputs to scr[j][lane].
 //
 // Two 32-particle groups per wave (g = 0: particles 0-31, g = 1: 32-63).  Both hidden layers
-// run on v_mfma_f32_32x32x2_f32 with the hidden unit on M and the particle on N; biases are
-// folded in as an extra K column fed a constant 1, so no accumulator is ever initialised.
+// run on v_mfma_f32_32x32x2_f32 with the hidden unit on M and the particle on N; b1 rides
+// as an extra K column fed a constant 1 (free for odd n_in), so no accumulator is initialised.
 //   layer 1: K = n_in + 1 (z, 1),  A = W1aug fragments, B = z of the lane's particle
-//   layer 2: K = 32 + 1 (h1, 1),   the layer-1 accumulator IS the B operand: register s of
-//            lane half h holds hidden row(s, h), so k-step s pairs rows (row(s,0), row(s,1))
-//            and the host packs W2 columns in that order.
+//   layer 2: K = 32,  the layer-1 accumulator IS the B operand: register s of lane half h
+//            holds hidden row(s, h), so k-step s pairs rows (row(s,0), row(s,1)) and the
+//            host packs W2 columns in that order; b2 is added after the transpose (SGPRs).
 //   head   : 16 v_permlane32_swap transpose the layer-2 accumulators so lane l holds all 32
 //            hidden units of particle l; the head then runs on VALU with wave-uniform weights.
 //
 // Parameter blocks (packed by vectorizedbayesiannetwork_amd/plan.py):
 //   off_std : mean_x[n_in], 1/std_x[n_in]                            (gaussian_nn only)
 //   off_w1  : [t][64]  lane l: W1aug[l&31][2t + (l>>5)],  W1aug = [W1 | b1 | 0]
-//   off_w2  : [q 5][lane 64][4], step s = 4q+e: s<16: W2[l&31][row(s, l>>5)];
-//             s = 16: (l>>5) == 0 ? b2[l&31] : 0;  s > 16: 0
+//   off_w2  : [q 4][lane 64][4], step s = 4q+e: W2[l&31][row(s, l>>5)]
+//   off_b2  : [32] = b2[row(r,0)] (r<16) ++ b2[row(r,1)]
 //   off_w3  : [n_out][32] = W3[j][row(r,0)] (r<16) ++ W3[j][row(r,1)]
 //   off_b3  : [n_out]
 // with row(r, h) = (r&3) + 8(r>>2) + 4h, the 32x32 accumulator row of register r, half h.
@@ -193,16 +202,15 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
   }
 
   const float4* w2p = reinterpret_cast<const float4*>(P + st.off_w2);
-  float w2[20];
+  float w2[16];
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
+  for (int q = 0; q < 4; ++q) {
     const float4 v = w2p[q * WAVE + lane];
     w2[4 * q + 0] = v.x;
     w2[4 * q + 1] = v.y;
     w2[4 * q + 2] = v.z;
     w2[4 * q + 3] = v.w;
   }
-  const float one = half ? 0.f : 1.f;
 
   f32x16 h2[2];
 #pragma unroll
@@ -219,21 +227,25 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
         a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
                                                  l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
     }
-    // layer 2 (+ bias step 16): the layer-1 accumulator is the B operand
+    // layer 2: the (activated) layer-1 accumulator is the B operand
+    float hb[16];
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) hb[s2] = act_fn<ACT>(a[s2]);
     f32x16 b = {};
 #pragma unroll
     for (int s2 = 0; s2 < 16; ++s2)
-      b = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[s2], act_fn<ACT>(a[s2]), b, 0, 0, 0);
-    h2[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[16], one, b, 0, 0, 0);
+      b = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[s2], hb[s2], b, 0, 0, 0);
+    h2[g] = b;
   }
 
-  // transpose: lane l <- all 32 hidden units of particle l
+  // transpose: lane l <- all 32 hidden units of particle l; + b2 (wave-uniform), activation
+  const float* __restrict__ b2 = P + st.off_b2;    // [32] = b2[row(r,0)] ++ b2[row(r,1)]
   float X[16], Y[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(h2[0][r]), __float_as_uint(h2[1][r]), false, false);
-    X[r] = act_fn<ACT>(__uint_as_float(sw[0]));   // hidden row(r, 0)
-    Y[r] = act_fn<ACT>(__uint_as_float(sw[1]));   // hidden row(r, 1)
+    X[r] = act_fn<ACT>(__uint_as_float(sw[0]) + b2[r]);        // hidden row(r, 0)
+    Y[r] = act_fn<ACT>(__uint_as_float(sw[1]) + b2[16 + r]);   // hidden row(r, 1)
   }
 
   // head (wave-uniform weights)
@@ -335,7 +347,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
     vwrite(L, st.out_col + d, x);
     if (want_lp) {
       const float diff = x - loc;
-      acc += (diff * diff) / (scale * scale) + 2.0f * logf(scale) + LOG_2PI_F;
+      acc += (diff * diff) / (scale * scale) + 2.0f * __logf(scale) + LOG_2PI_F;
     }
   }
   if (want_lp) lp += -0.5f * acc;
@@ -417,14 +429,14 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
     lmax = -INFINITY;
     for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, scr[k * WAVE + lane]);
     lsum = 0.f;
-    for (int k = 0; k < K; ++k) lsum += expf(scr[k * WAVE + lane] - lmax);
+    for (int k = 0; k < K; ++k) lsum += __expf(scr[k * WAVE + lane] - lmax);
     psum = 0.f;
-    for (int k = 0; k < K; ++k) psum += fmaxf(expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f);
+    for (int k = 0; k < K; ++k) psum += fmaxf(__expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f);
     psum = fmaxf(psum, 1e-12f);
   }
   auto pi_k = [&](int k) -> float {
     if (root) return t[k];
-    return fmaxf(expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f) / psum;
+    return fmaxf(__expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f) / psum;
   };
   auto loc_kd = [&](int k, int d) -> float {
     return root ? t[2 * K + k * D + d] : scr[(K + k * 2 * D + d) * WAVE + lane];
@@ -455,23 +467,23 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
           ls = t[2 * K + 2 * K * D + k * D + d];
           var = t[2 * K + 3 * K * D + k * D + d];
         } else {
-          ls = logf(scale_kd(k, d));
-          var = expf(2.0f * ls);
+          ls = __logf(scale_kd(k, d));
+          var = __expf(2.0f * ls);
         }
         const float diff = x - loc_kd(k, d);
         acc += (diff * diff) / var + 2.0f * ls + LOG_2PI_F;
       }
-      const float lpi = root ? t[K + k] : logf(pi_k(k));
+      const float lpi = root ? t[K + k] : __logf(pi_k(k));
       const float term = lpi + (-0.5f * acc);
       if (term == -INFINITY) continue;
       if (term > m) {
-        se = se * expf(m - term) + 1.0f;
+        se = se * __expf(m - term) + 1.0f;
         m = term;
       } else {
-        se += expf(term - m);
+        se += __expf(term - m);
       }
     }
-    lp += (m == -INFINITY) ? m : m + logf(se);
+    lp += (m == -INFINITY) ? m : m + __logf(se);
   }
 }
 
@@ -507,14 +519,14 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
     float m = -INFINITY;
     for (int c = 0; c < C; ++c) m = fmaxf(m, logit(c));
     float se = 0.f;
-    for (int c = 0; c < C; ++c) se += expf(logit(c) - m);
+    for (int c = 0; c < C; ++c) se += __expf(logit(c) - m);
     const bool disc = (st.aux1 >> d) & 1;
     const float* e = edges + d * (C + 1);
     float x;
     int idx;
     if (latent) {
       const Draw r = get_draw(A, st, d, L);
-      idx = inv_cdf(C, r.ucat, [&](int c) { return expf(logit(c) - m) / se; });
+      idx = inv_cdf(C, r.ucat, [&](int c) { return __expf(logit(c) - m) / se; });
       const float left = e[idx];
       const float right = e[idx + 1 < C ? idx + 1 : C];
       const float width = fmaxf(right - left, min_bw);
@@ -551,7 +563,7 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
         for (int c = 0; c <= C; ++c) cnt += (x >= e[c]) ? 1 : 0;
         bin = min(max(cnt - 1, 0), C - 1);
       }
-      const float log_bin = logit(bin) - m - logf(se);
+      const float log_bin = logit(bin) - m - __logf(se);
       float lw = 0.f;
       if (!disc) {
         const float left = e[bin];
@@ -802,7 +814,7 @@ __global__ void __launch_bounds__(WAVE) vbn_walk_kernel(const vbn_walk_args A, c
     wave_sync();
   }
   if (!valid) return;
-  if (A.out_lp && A.mode != VBN_MODE_SAMPLE) A.out_lp[L.p] = (A.mode == VBN_MODE_MCM) ? expf(lp) : lp;
+  if (A.out_lp && A.mode != VBN_MODE_SAMPLE) A.out_lp[L.p] = (A.mode == VBN_MODE_MCM) ? __expf(lp) : lp;
   if (A.out_x) {
     for (int k = 0; k < A.n_out_cols; ++k)
       A.out_x[L.p * A.n_out_cols + k] = vread(L, A.out_cols[k]);
@@ -895,8 +907,8 @@ extern "C" int vbn_hip_abi_version(void) { return VBN_ABI_VERSION; }
 extern "C" const char* vbn_hip_last_error(void) { return g_err; }
 
 extern "C" int64_t vbn_hip_lds_bytes(int32_t n_slots, int32_t max_out) {
-  const int32_t scr = max_out > KDE_CHUNKS ? max_out : KDE_CHUNKS;
-  return (int64_t)(n_slots + scr) * WAVE * (int64_t)sizeof(float);
+  // the host sizes max_out >= KDE_CHUNKS when the plan walks a KDE node (chunk sums)
+  return (int64_t)(n_slots + (max_out > 0 ? max_out : 1)) * WAVE * (int64_t)sizeof(float);
 }
 
 extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {

@@ -96,11 +96,11 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     lane = np.arange(64)
     w1f = np.stack([w1aug[lane & 31, 2 * t + (lane >> 5)] for t in range(t1)])   # [t1, 64]
     offs["w1"] = blob.add(w1f)
-    w2f = np.zeros((20, 64), np.float32)
+    w2f = np.zeros((16, 64), np.float32)
     for s in range(16):
         w2f[s] = w2[lane & 31, _ROWS[lane >> 5, s]]
-    w2f[16] = np.where(lane < 32, b2[lane & 31], 0.0)
-    offs["w2"] = blob.add(w2f.reshape(5, 4, 64).transpose(0, 2, 1))            # [5, 64, 4]
+    offs["w2"] = blob.add(w2f.reshape(4, 4, 64).transpose(0, 2, 1))            # [4, 64, 4]
+    offs["b2"] = blob.add(np.concatenate([b2[_ROWS[0]], b2[_ROWS[1]]]))        # [32]
     offs["w3"] = blob.add(np.concatenate([w3[:, _ROWS[0]], w3[:, _ROWS[1]]], axis=1))  # [n_out, 32]
     offs["b3"] = blob.add(b3)
     offs["n_out"] = w3.shape[0]
