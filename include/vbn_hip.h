@@ -113,6 +113,8 @@ typedef struct vbn_walk_args {
 
 int vbn_hip_abi_version(void);
 const char* vbn_hip_last_error(void);
+/* sizeof(vbn_walk_args) for which = 0, sizeof(vbn_step) for which = 1 (binding checks) */
+int vbn_hip_struct_size(int which);
 
 /* Topological particle walk (see header comment). */
 int vbn_hip_walk(const vbn_walk_args* args, void* stream);

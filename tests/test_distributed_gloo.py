@@ -1,0 +1,104 @@
+"""Query-sharded multi-process path on CPU (gloo, world_size 2).
+
+The local engine is a deterministic CPU stand-in with the accelerated engines' interface
+(``q_base`` + ``seed`` + optional ``_reduce_flag``), so the test checks the sharding,
+seed broadcast, batch-global fallback decision and the gather exactly.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from vectorizedbayesiannetwork_amd.distributed import ShardedEngine, shard_bounds
+from vectorizedbayesiannetwork_amd.engines import Query
+
+S = 6
+
+
+class StubEngine:
+    """pdf[b, s] depends on (global query, sample, seed); a 'fallback' flips the sign when any
+    query of the WHOLE batch has evidence > 10 (batch-global decision, like IS -> LW)."""
+
+    def __init__(self):
+        self.q_base = 0
+        self.last_fallback = None
+
+    def infer_posterior(self, vbn, query, seed=None, _reduce_flag=None, **kw):
+        ev = query.evidence["x"]
+        b = ev.shape[0]
+        q = torch.arange(self.q_base, self.q_base + b, dtype=torch.float64).unsqueeze(1)
+        s = torch.arange(S, dtype=torch.float64).unsqueeze(0)
+        pdf = torch.sin(q * 1.7 + s * 0.3 + (seed % 1000) * 1e-3).float()
+        flag = (ev > 10).any()
+        if _reduce_flag is not None:
+            flag = _reduce_flag(flag)
+        self.last_fallback = bool(flag)
+        if bool(flag):
+            pdf = -pdf
+        return pdf, (pdf.unsqueeze(-1) + ev.unsqueeze(1))
+
+
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def _worker(rank, world, port, ev, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(123 + rank)                 # ranks disagree; the seed is broadcast
+        eng = ShardedEngine(StubEngine(), gather=True)
+        pdf, xs = eng.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}))
+        out_q.put((rank, None if pdf is None else pdf.clone(), None if xs is None else xs.clone(),
+                   eng.engine.last_fallback))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(ev, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, ev, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    return sorted(res, key=lambda r: r[0])
+
+
+def test_shard_bounds_cover_batch():
+    for n in (2, 5, 8, 4096, 4097):
+        for w in (1, 2, 3, 8):
+            if n < w:
+                continue
+            spans = [shard_bounds(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("hot", [False, True])
+def test_gloo_world2_matches_single_process(hot):
+    ev = torch.linspace(-1, 1, 7).unsqueeze(1)
+    if hot:
+        ev[6, 0] = 50.0                               # only rank 1 sees it; fallback is global
+    res = _run(ev)
+    (r0, pdf, xs, fb0), (r1, pdf1, xs1, fb1) = res
+    assert pdf1 is None and xs1 is None                # gathered on rank 0 only
+    assert fb0 == fb1 == hot
+    # single-process reference with the seed rank 0 broadcast
+    torch.manual_seed(123)
+    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    ref = StubEngine()
+    rpdf, rxs = ref.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}), seed=seed)
+    assert torch.equal(pdf, rpdf)
+    assert torch.equal(xs, rxs)

@@ -1,0 +1,172 @@
+"""Host-side plan logic: liveness slot allocation and MFMA fragment packing.
+
+``emulate_mlp`` replays csrc/vbn_walk.hip's mlp_forward data flow in numpy with the
+documented gfx950 lane layouts of v_mfma_f32_32x32x2_f32 (A[i=l&31][k=l>>5],
+B[k=l>>5][j=l&31], D row (r&3)+8(r>>2)+4(l>>5), col l&31) and v_permlane32_swap, so the
+packed parameter blocks are checked against torch's MLP without a GPU.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_names, load_golden
+from vectorizedbayesiannetwork_amd import synthetic
+from vectorizedbayesiannetwork_amd.model import model_from_checkpoint, random_init_model
+from vectorizedbayesiannetwork_amd.plan import (F_LOGP, MODE_MCM, MODE_WEIGHTED, ROLE_FIXED, ROLE_LATENT,
+                                                S_INOFF, S_NIN, S_OFF_B2, S_OFF_B3, S_OFF_STD, S_OFF_W1,
+                                                S_OFF_W2, S_OFF_W3, S_OUTCOL, S_OUTDIM, S_ROLE, S_FLAGS,
+                                                PackedModel, build_plan)
+
+
+def _row(r, h):
+    return (r & 3) + 8 * (r >> 2) + 4 * h
+
+
+def mfma_32x32x2(a_lane, b_lane, c):
+    """a_lane, b_lane: [64]; c: [64,16] (lane, reg) -> d [64,16]."""
+    A = np.zeros((32, 2)); B = np.zeros((2, 32))
+    for l in range(64):
+        A[l & 31, l >> 5] = a_lane[l]
+        B[l >> 5, l & 31] = b_lane[l]
+    D = A.astype(np.float64) @ B
+    d = c.astype(np.float64).copy()
+    for l in range(64):
+        for r in range(16):
+            d[l, r] += D[_row(r, l >> 5), l & 31]
+    return d
+
+
+def permlane32_swap(vdst, vsrc):
+    a, b = vdst.copy(), vsrc.copy()
+    a[32:], b[:32] = vsrc[:32].copy(), vdst[32:].copy()
+    return a, b
+
+
+def emulate_mlp(P, row, parents64, std):
+    """parents64: [nin, 64] values of the 64 particles of a wave -> head [n_out, 64]."""
+    nin = row[S_NIN]
+    t1 = (nin + 2) // 2
+    lanes = np.arange(64)
+    half, c = lanes >> 5, lanes & 31
+    h2 = []
+    for g in range(2):
+        acc = np.zeros((64, 16))
+        for t in range(t1):
+            kk = 2 * t + half
+            z = np.zeros(64)
+            for l in range(64):
+                if kk[l] < nin:
+                    v = parents64[kk[l], c[l] + 32 * g]
+                    if std:
+                        v = (v - P[row[S_OFF_STD] + kk[l]]) * P[row[S_OFF_STD] + nin + kk[l]]
+                    z[l] = v
+                elif kk[l] == nin:
+                    z[l] = 1.0
+            acc = mfma_32x32x2(P[row[S_OFF_W1] + t * 64: row[S_OFF_W1] + t * 64 + 64], z, acc)
+        hb = np.maximum(acc, 0)
+        w2 = P[row[S_OFF_W2]: row[S_OFF_W2] + 1024].reshape(4, 64, 4)
+        b = np.zeros((64, 16))
+        for s in range(16):
+            b = mfma_32x32x2(w2[s // 4, :, s % 4], hb[:, s], b)
+        h2.append(b)
+    b2 = P[row[S_OFF_B2]: row[S_OFF_B2] + 32]
+    X = np.zeros((64, 16)); Y = np.zeros((64, 16))
+    for r in range(16):
+        x, y = permlane32_swap(h2[0][:, r], h2[1][:, r])
+        X[:, r] = np.maximum(x + b2[r], 0)
+        Y[:, r] = np.maximum(y + b2[16 + r], 0)
+    n_out = row[10]
+    w3 = P[row[S_OFF_W3]: row[S_OFF_W3] + 32 * n_out].reshape(n_out, 32)
+    b3 = P[row[S_OFF_B3]: row[S_OFF_B3] + n_out]
+    return (X @ w3[:, :16].T + Y @ w3[:, 16:].T + b3).T
+
+
+@pytest.mark.parametrize("name", ["readme", "family_gaussian_nn", "family_mdn", "mix12"])
+def test_mfma_fragment_packing_reproduces_torch_mlp(name):
+    model = model_from_checkpoint(load_golden(name)["model"])
+    pk = PackedModel(model, torch.device("cpu"))
+    P = pk.params.numpy().astype(np.float64)
+    rng = np.random.default_rng(0)
+    checked = 0
+    for node in model.topo:
+        rec = model.cpds[node]
+        if rec.kind not in ("gaussian_nn", "mdn", "softmax_nn") or rec.is_root:
+            continue
+        plan = build_plan(pk, latent=[node], fixed=model.parents[node], logp=[], out_nodes=[node],
+                          shared_roots=False, mode=MODE_WEIGHTED,
+                          skip=[n for n in model.topo if n != node and n not in model.parents[node]])
+        row = plan.steps[-1].numpy()
+        parents64 = rng.normal(size=(rec.input_dim, 64))
+        std = rec.kind == "gaussian_nn"
+        got = emulate_mlp(P, row, parents64, std)
+        x = torch.tensor(parents64.T, dtype=torch.float64)
+        if std:
+            x = (x - rec.state["mean_x"].double()) / rec.state["std_x"].double()
+        h = x
+        layers = rec.mlp_layers()
+        for i, (w, b) in enumerate(layers):
+            h = h @ w.double().t() + b.double()
+            if i + 1 < len(layers):
+                h = torch.relu(h)
+        np.testing.assert_allclose(got, h.numpy().T, rtol=1e-5, atol=1e-5)
+        checked += 1
+    assert checked > 0
+
+
+def _check_liveness(model, plan):
+    """Replay the slot writes; every read must find the right parent's value."""
+    steps = plan.steps.numpy()
+    in_cols = plan.in_cols.numpy()
+    holder = {}
+    order = [n for n in model.topo if n in plan.slot_of]
+    for i, node in enumerate(order):
+        row = steps[i]
+        reads = row[S_ROLE] == ROLE_LATENT or (row[S_FLAGS] & F_LOGP)
+        if reads:
+            cols = in_cols[row[S_INOFF]: row[S_INOFF] + row[S_NIN]]
+            expect = []
+            for p in model.parents[node]:
+                expect += [(p, d) for d in range(model.out_dim(p))]
+            assert [holder.get(int(c)) for c in cols] == expect, (node, cols)
+        for d in range(row[S_OUTDIM]):
+            holder[int(row[S_OUTCOL] + d)] = (node, d)
+        assert row[S_OUTCOL] + row[S_OUTDIM] <= plan.n_slots
+    outs = plan.out_cols.numpy()
+    want = []
+    for n in plan.out_nodes:
+        want += [(n, d) for d in range(model.out_dim(n))]
+    assert [holder.get(int(c)) for c in outs] == want
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_liveness_slots_never_clobber_live_values(name):
+    model = model_from_checkpoint(load_golden(name)["model"])
+    pk = PackedModel(model, torch.device("cpu"))
+    topo = model.topo
+    for k in range(0, len(topo), 2):
+        ev = topo[:k:3]
+        target = topo[-1 - (k % 3)]
+        latent = [n for n in topo if n not in ev]
+        plan = build_plan(pk, latent=latent, fixed=ev, logp=[target] + ev, out_nodes=[target],
+                          shared_roots=True, mode=MODE_MCM)
+        _check_liveness(model, plan)
+        joint = build_plan(pk, latent=latent, fixed=ev, logp=[], out_nodes=list(topo),
+                           shared_roots=True, mode=MODE_MCM)
+        _check_liveness(model, joint)
+        assert joint.n_slots == sum(model.out_dim(n) for n in topo)
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "anchor64", "cfg5"])
+def test_bench_configs_pack(cfg):
+    c = synthetic.CONFIGS[cfg]
+    g = synthetic.random_dag(c["n_nodes"], seed=0)
+    data = synthetic.sem_data(g, 300, seed=0)
+    model = random_init_model(g, synthetic.round_robin_kinds(g, c["kinds"]), data,
+                              overrides={"kde": {"max_points": 64}})
+    pk = PackedModel(model, torch.device("cpu"))
+    target, ev = synthetic.default_query_nodes(g, seed=1)
+    plan = build_plan(pk, latent=[n for n in model.topo if n not in ev], fixed=ev, logp=[target],
+                      out_nodes=[target], shared_roots=True, mode=MODE_MCM)
+    _check_liveness(model, plan)
+    assert plan.n_slots < len(model.topo)               # liveness reuses slots
+    assert (plan.steps[:, S_ROLE] == ROLE_FIXED).sum() == len(ev)

@@ -21,6 +21,7 @@ EXPORTS = (
     "vbn_hip_walk",
     "vbn_hip_normalize_weights",
     "vbn_hip_lds_bytes",
+    "vbn_hip_struct_size",
 )
 
 
@@ -90,6 +91,10 @@ def load(path: str = None) -> ctypes.CDLL:
         lib.vbn_hip_normalize_weights.restype = ctypes.c_int
         lib.vbn_hip_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
         lib.vbn_hip_lds_bytes.restype = ctypes.c_int64
+        lib.vbn_hip_struct_size.argtypes = [ctypes.c_int]
+        lib.vbn_hip_struct_size.restype = ctypes.c_int
+        if lib.vbn_hip_struct_size(0) != ctypes.sizeof(VbnWalkArgs) or lib.vbn_hip_struct_size(1) != 128:
+            raise VbnHipError(f"{p}: struct layout differs from the ctypes mirror")
         v = lib.vbn_hip_abi_version()
         if v != ABI_VERSION:
             raise VbnHipError(f"{p}: ABI version {v}, expected {ABI_VERSION}")

@@ -191,7 +191,6 @@ template <int ACT, bool STD, int NIN>
 __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
   const float* __restrict__ P = L.P;
   const int lane = L.lane;
-  const int half = lane >> 5;
   const int nin = NIN > 0 ? NIN : st.n_in;
   const int t1 = (nin + 2) >> 1;                  // layer-1 k-steps incl. the bias column
 
@@ -904,6 +903,9 @@ static int fail(int code, const char* msg) {
 }
 
 extern "C" int vbn_hip_abi_version(void) { return VBN_ABI_VERSION; }
+extern "C" int vbn_hip_struct_size(int which) {
+  return which == 0 ? (int)sizeof(vbn_walk_args) : (which == 1 ? (int)sizeof(vbn_step) : -1);
+}
 extern "C" const char* vbn_hip_last_error(void) { return g_err; }
 
 extern "C" int64_t vbn_hip_lds_bytes(int32_t n_slots, int32_t max_out) {

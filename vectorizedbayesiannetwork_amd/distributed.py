@@ -1,0 +1,138 @@
+"""Query-sharded data parallelism: one process per GPU over ``torch.distributed``.
+
+Queries are independent, so the batch is split into contiguous shards and each rank walks
+its own shard with no data-path collective.  Two things keep the result
+identical to a single-GPU run of the whole batch:
+
+* every rank uses the same RNG seed (broadcast from rank 0 once per call) and its shard's
+  global query offset (``q_base``) keys the per-query Philox streams; root-node draws that
+  the reference shares across the batch (Q5) are keyed without the query and so agree;
+* the importance-sampling fallback stays batch-global (Q6): the per-rank "any ESS below
+  threshold" flag is all-reduced with MAX (a 4-byte RCCL all-reduce) before deciding.
+
+``gather=True`` additionally collects pdf/samples on ``dst`` (RCCL gather over xGMI).
+The same code runs on ``gloo`` for CPU tests (with a CPU stand-in engine).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .engines import Query, infer_batch_size
+
+__all__ = ["shard_bounds", "shard_query", "ShardedEngine"]
+
+
+def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous, balanced [b0, b1) of ``n`` queries for ``rank`` (first n % world ranks +1)."""
+    q, r = divmod(n, world)
+    b0 = rank * q + min(rank, r)
+    return b0, b0 + q + (1 if rank < r else 0)
+
+
+def shard_query(query, b0: int, b1: int) -> Query:
+    ev = {k: v[b0:b1] for k, v in (query.evidence or {}).items()}
+    do = {k: v[b0:b1] for k, v in (getattr(query, "do", None) or {}).items()}
+    return Query(target=query.target, evidence=ev, do=do)
+
+
+def _world(group) -> Tuple[int, int]:
+    if not dist.is_available() or not dist.is_initialized():
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+class ShardedEngine:
+    """Wrap an engine (``infer_posterior`` or ``sample``) for query-sharded multi-GPU runs."""
+
+    def __init__(self, engine, group=None, gather: bool = False, dst: int = 0):
+        self.engine = engine
+        self.group = group
+        self.gather = bool(gather)
+        self.dst = int(dst)
+
+    def _device(self):
+        backend = dist.get_backend(self.group) if dist.is_initialized() else "gloo"
+        if backend == "nccl":
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    def _shared_seed(self, kwargs) -> int:
+        if kwargs.get("seed") is not None:
+            return int(kwargs["seed"])
+        rank, world = _world(self.group)
+        s = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
+        if world > 1:
+            s = s.to(self._device())
+            dist.broadcast(s, src=0, group=self.group)
+        return int(s.item())
+
+    def _flag_reducer(self):
+        rank, world = _world(self.group)
+        if world == 1:
+            return None
+        dev = self._device()
+
+        def reduce(flag: torch.Tensor) -> torch.Tensor:
+            f = flag.to(device=dev, dtype=torch.int32).reshape(1)
+            dist.all_reduce(f, op=dist.ReduceOp.MAX, group=self.group)
+            return f[0] > 0
+        return reduce
+
+    def _set_base(self, b0: int) -> None:
+        self.engine.q_base = b0
+        lw = getattr(self.engine, "_lw", None)
+        if lw is not None:
+            lw.q_base = b0
+
+    def _gather(self, t: torch.Tensor, n_total: int) -> Optional[torch.Tensor]:
+        rank, world = _world(self.group)
+        b0, b1 = shard_bounds(n_total, rank, world)
+        if world == 1 or t.shape[0] != b1 - b0:     # e.g. MCM root target: (1, S) on every rank
+            return t
+        dev = self._device()
+        q_max = -(-n_total // world)
+        pad = torch.zeros((q_max,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        pad[: t.shape[0]] = t.to(dev)
+        parts = [torch.empty_like(pad) for _ in range(world)] if rank == self.dst else None
+        dist.gather(pad, parts, dst=self.dst, group=self.group)
+        if rank != self.dst:
+            return None
+        out = [parts[r][: shard_bounds(n_total, r, world)[1] - shard_bounds(n_total, r, world)[0]]
+               for r in range(world)]
+        return torch.cat(out, dim=0)
+
+    def _check(self, n_total: int, world: int) -> None:
+        if n_total < world:
+            raise ValueError(f"{n_total} queries cannot be sharded over {world} ranks")
+
+    def infer_posterior(self, vbn, query, **kwargs):
+        rank, world = _world(self.group)
+        n_total = infer_batch_size(query.evidence, getattr(query, "do", None))
+        self._check(n_total, world)
+        b0, b1 = shard_bounds(n_total, rank, world)
+        self._set_base(b0)
+        kw = dict(kwargs)
+        kw["seed"] = self._shared_seed(kwargs)
+        red = self._flag_reducer()
+        if red is not None:
+            kw["_reduce_flag"] = red
+        pdf, xs = self.engine.infer_posterior(vbn, shard_query(query, b0, b1), **kw)
+        if not self.gather:
+            return pdf, xs
+        return self._gather(pdf, n_total), self._gather(xs, n_total)
+
+    def sample(self, vbn, query, n_samples=None, **kwargs):
+        rank, world = _world(self.group)
+        n_total = infer_batch_size(query.evidence, getattr(query, "do", None))
+        self._check(n_total, world)
+        b0, b1 = shard_bounds(n_total, rank, world)
+        self._set_base(b0)
+        kw = dict(kwargs)
+        kw["seed"] = self._shared_seed(kwargs)
+        xs = self.engine.sample(vbn, shard_query(query, b0, b1), n_samples, **kw)
+        if not self.gather or isinstance(xs, dict):
+            return xs
+        return self._gather(xs, n_total)

@@ -201,7 +201,7 @@ def record_from_cpd(cpd: Any, kind: Optional[str] = None) -> CPDRecord:
     if kind is None:
         raise ValueError(f"CPD class '{type(cpd).__name__}' is not on the accelerated path")
     init_kwargs = cpd.get_init_kwargs() if hasattr(cpd, "get_init_kwargs") else {}
-    extra = cpd.get_extra_state() if hasattr(cpd, "get_extra_state") else None
+    extra = _extra_of(cpd)
     return CPDRecord(
         kind=kind,
         input_dim=int(cpd.input_dim),
@@ -212,12 +212,23 @@ def record_from_cpd(cpd: Any, kind: Optional[str] = None) -> CPDRecord:
     )
 
 
+def _extra_of(cpd: Any) -> Any:
+    """BaseCPD.get_extra_state (core/base.py:75-77); a bare nn.Module's default raises."""
+    fn = getattr(cpd, "get_extra_state", None)
+    if fn is None:
+        return None
+    try:
+        return fn()
+    except RuntimeError:
+        return None
+
+
 def _tensor_fingerprint(cpd: Any) -> Tuple:
     fp = []
     for t in cpd.state_dict(keep_vars=True).values():
         if isinstance(t, torch.Tensor):
             fp.append((t.data_ptr(), t._version))
-    extra = cpd.get_extra_state() if hasattr(cpd, "get_extra_state") else None
+    extra = _extra_of(cpd)
     if isinstance(extra, Mapping):
         for v in extra.values():
             if isinstance(v, torch.Tensor):
