@@ -24,7 +24,7 @@ def main():
                        max_ns=float(r["MaxNs"]), pct=float(r["Percentage"]))
     trace = list(csv.DictReader(open(f"{d}/trace/run_kernel_trace.csv")))
     big = [int(t["End_Timestamp"]) - int(t["Start_Timestamp"]) for t in trace
-           if kname in t["Kernel_Name"] and int(t.get("Grid_Size", 0) or 0) >= 4096 * 64]
+           if kname in t["Kernel_Name"] and int(t.get("Grid_Size_X", 0) or 0) >= 4096 * 64]
     if big:
         res["avg_ns_full_size"] = sum(big) / len(big)
     pmc = collections.defaultdict(list)

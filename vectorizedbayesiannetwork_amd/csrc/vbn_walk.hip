@@ -34,6 +34,10 @@
 #define LOG_2PI_F 1.8378770664093453f
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// step field holding the split-f16 W2 fragments (vbn_step.reserved[0])
+#define OFF_W2H(st) ((st).reserved[0])
 
 // ------------------------------------------------------------------------------------------
 // small device helpers
@@ -151,16 +155,23 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
 // run on v_mfma_f32_32x32x2_f32 with the hidden unit on M and the particle on N; b1 rides
 // as an extra K column fed a constant 1 (free for odd n_in), so no accumulator is initialised.
 //   layer 1: K = n_in + 1 (z, 1),  A = W1aug fragments, B = z of the lane's particle
-//   layer 2: K = 32,  the layer-1 accumulator IS the B operand: register s of lane half h
-//            holds hidden row(s, h), so k-step s pairs rows (row(s,0), row(s,1)) and the
-//            host packs W2 columns in that order; b2 is added after the transpose (SGPRs).
+//   layer 2: K = 32 on v_mfma_f32_32x32x16_f16 as a 3-pass split product: x = hi + lo with
+//            hi = f16(x), lo = f16(x - hi) for both operands; A_lo.B_hi + A_hi.B_lo + A_hi.B_hi
+//            accumulated in f32 (relative error ~2^-22 per product, i.e. fp32-level) at 1/5
+//            of the f32-MFMA time.  The layer-1 accumulator IS the B operand: register 8s+j
+//            of lane half h holds hidden row 16s + 8(j>>2) + 4h + (j&3), and the host packs
+//            W2 in that k order.  If any |h| > 32768 (f16 range) the wave takes the exact
+//            f32 chain (v_mfma_f32_32x32x2_f32, k-step s pairs rows (row(s,0), row(s,1))).
+//            b2 is added after the transpose (SGPRs).
 //   head   : 16 v_permlane32_swap transpose the layer-2 accumulators so lane l holds all 32
 //            hidden units of particle l; the head then runs on VALU with wave-uniform weights.
 //
 // Parameter blocks (packed by vectorizedbayesiannetwork_amd/plan.py):
 //   off_std : mean_x[n_in], 1/std_x[n_in]                            (gaussian_nn only)
 //   off_w1  : [t][64]  lane l: W1aug[l&31][2t + (l>>5)],  W1aug = [W1 | b1 | 0]
-//   off_w2  : [q 4][lane 64][4], step s = 4q+e: W2[l&31][row(s, l>>5)]
+//   off_w2  : [q 4][lane 64][4], step s = 4q+e: W2[l&31][row(s, l>>5)]   (f32 fallback)
+//   off_w2h : [4][lane 64][8 f16]: hi(s=0), hi(s=1), lo(s=0), lo(s=1);
+//             element j of lane l: W2[l&31][16s + 8(j>>2) + 4(l>>5) + (j&3)]
 //   off_b2  : [32] = b2[row(r,0)] (r<16) ++ b2[row(r,1)]
 //   off_w3  : [n_out][32] = W3[j][row(r,0)] (r<16) ++ W3[j][row(r,1)]
 //   off_b3  : [n_out]
@@ -200,17 +211,16 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
     nan_in |= (v != v);
   }
 
-  const float4* w2p = reinterpret_cast<const float4*>(P + st.off_w2);
-  float w2[16];
+  // layer-2 A fragments, split f16 (hi, lo) for the two K=16 steps (see header)
+  const uint4* w2h = reinterpret_cast<const uint4*>(P + OFF_W2H(st));
+  f16x8 ah[2], al[2];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 v = w2p[q * WAVE + lane];
-    w2[4 * q + 0] = v.x;
-    w2[4 * q + 1] = v.y;
-    w2[4 * q + 2] = v.z;
-    w2[4 * q + 3] = v.w;
+  for (int s2 = 0; s2 < 2; ++s2) {
+    ah[s2] = __builtin_bit_cast(f16x8, w2h[s2 * WAVE + lane]);
+    al[s2] = __builtin_bit_cast(f16x8, w2h[(2 + s2) * WAVE + lane]);
   }
 
+  f16x8 bh[2], bl[2];
   f32x16 h2[2];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
@@ -226,14 +236,45 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
         a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
                                                  l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
     }
-    // layer 2: the (activated) layer-1 accumulator is the B operand
     float hb[16];
+    unsigned big = 0;
 #pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2) hb[s2] = act_fn<ACT>(a[s2]);
+    for (int r = 0; r < 16; ++r) {
+      hb[r] = act_fn<ACT>(a[r]);
+      big = max(big, (unsigned)__float_as_int(hb[r]) & 0x7fffffffu);   // |h| as ordered bits; NaN counts as big
+    }
     f32x16 b = {};
+    if (!(st.flags & VBN_F_F32L2) && !__any(big > 0x47000000u)) {  // |h| <= 32768: in f16 split range
+      // layer 2 as three f16 MFMAs per K=16 step: A_lo.B_hi + A_hi.B_lo + A_hi.B_hi (f32 accumulate).
+      // B operand: register 8s+j of lane half h holds hidden row 16s + 8(j>>2) + 4h + (j&3).
 #pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2)
-      b = __builtin_amdgcn_mfma_f32_32x32x2f32(w2[s2], hb[s2], b, 0, 0, 0);
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = hb[8 * s2 + j];
+          const _Float16 hi = (_Float16)x;
+          bh[s2][j] = hi;
+          bl[s2][j] = (_Float16)(x - (float)hi);
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s2], bh[s2], b, 0, 0, 0);
+        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2], bl[s2], b, 0, 0, 0);
+        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2], bh[s2], b, 0, 0, 0);
+      }
+    } else {
+      // exact f32 chain (K = 32 as 16 steps of 2), W2 fragments in off_w2
+      const float4* w2p = reinterpret_cast<const float4*>(P + st.off_w2);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = w2p[q * WAVE + lane];
+        b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, hb[4 * q + 0], b, 0, 0, 0);
+        b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, hb[4 * q + 1], b, 0, 0, 0);
+        b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, hb[4 * q + 2], b, 0, 0, 0);
+        b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, hb[4 * q + 3], b, 0, 0, 0);
+      }
+    }
     h2[g] = b;
   }
 

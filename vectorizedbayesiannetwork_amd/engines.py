@@ -205,12 +205,16 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
 
 class _EngineBase:
     def __init__(self, n_samples: int = 200, seed: Optional[int] = None, prune_barren: bool = False,
-                 q_base: int = 0, **kwargs):
+                 q_base: int = 0, exact_f32: bool = False, **kwargs):
         self.n_samples = int(n_samples)
         self.seed = seed
         self.prune_barren = bool(prune_barren)
         self.q_base = int(q_base)
+        self.exact_f32 = bool(exact_f32)     # hidden layer on the exact f32 MFMA chain
         self._calls = 0
+
+    def _plan(self, pk, key, **kw):
+        return _plan(pk, key + (self.exact_f32,), exact_f32=self.exact_f32, **kw)
 
     def _seed(self, kwargs) -> int:
         if "seed" in kwargs and kwargs["seed"] is not None:
@@ -251,7 +255,7 @@ class MonteCarloMarginalization(_EngineBase):
             t_fixed = target in vals
             nodes = set(parents) | {target}
             key = ("mcm-short", target, t_fixed)
-            plan = _plan(pk, key, latent=[] if t_fixed else [target],
+            plan = self._plan(pk, key, latent=[] if t_fixed else [target],
                          fixed=[x for x in model.topo if x in nodes and x != target] + ([target] if t_fixed else []),
                          logp=[target], out_nodes=[target], shared_roots=True, mode=MODE_MCM,
                          skip=[x for x in model.topo if x not in nodes])
@@ -259,7 +263,7 @@ class MonteCarloMarginalization(_EngineBase):
         else:
             keep = barren_pruned(model, [target]) if prune else set(model.topo)
             key = ("mcm", target, tuple(sorted(vals)), prune)
-            plan = _plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
+            plan = self._plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
                          fixed=[x for x in fixed if x in keep], logp=[target], out_nodes=[target],
                          shared_roots=True, mode=MODE_MCM, skip=[x for x in model.topo if x not in keep])
             b_eff = b
@@ -288,7 +292,7 @@ class LikelihoodWeighting(_EngineBase):
         _check_discrete(pk, vals, list(ev))
         keep = barren_pruned(model, [target] + list(ev)) if self.prune_barren else set(model.topo)
         key = ("weighted", target, tuple(sorted(ev)), tuple(sorted(do)), shared_roots, self.prune_barren)
-        plan = _plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
+        plan = self._plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
                      fixed=[x for x in model.topo if x in keep and x in vals],
                      logp=[x for x in model.topo if x in ev and x in keep], out_nodes=[target],
                      shared_roots=shared_roots, mode=MODE_WEIGHTED,
@@ -320,7 +324,8 @@ class ImportanceSampling(LikelihoodWeighting):
         self.ess_threshold = 0.1
         self._last_fallback = False
         self._last_ess: Optional[torch.Tensor] = None
-        self._lw = LikelihoodWeighting(n_samples=self.n_samples, q_base=self.q_base)
+        self._lw = LikelihoodWeighting(n_samples=self.n_samples, q_base=self.q_base,
+                                       exact_f32=self.exact_f32)
 
     def fallback_needed(self, ess: torch.Tensor, n: int) -> torch.Tensor:
         """Device-side flag (NaN ESS never triggers; importance_sampling.py:85-86)."""
@@ -362,7 +367,7 @@ class AncestralSampler(_EngineBase):
         outs = [target] if target else list(model.topo)
         keep = barren_pruned(model, outs) if (self.prune_barren and target) else set(model.topo)
         key = ("ancestral", target, tuple(sorted(vals)), self.prune_barren and bool(target))
-        plan = _plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
+        plan = self._plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
                      fixed=[x for x in model.topo if x in keep and x in vals], logp=[],
                      out_nodes=outs, shared_roots=True, mode=MODE_SAMPLE,
                      skip=[x for x in model.topo if x not in keep])

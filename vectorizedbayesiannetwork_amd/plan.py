@@ -29,14 +29,14 @@ from .model import BNModel, CPDRecord
 # ---- must match include/vbn_hip.h -------------------------------------------------------
 KIND_ID = {"gaussian_nn": 0, "linear_gaussian": 1, "mdn": 2, "kde": 3, "softmax_nn": 4}
 ROLE_SKIP, ROLE_LATENT, ROLE_FIXED = 0, 1, 2
-F_LOGP, F_ROOT, F_SHARED, F_STANDARDIZE, F_CLIP = 1, 2, 4, 8, 16
+F_LOGP, F_ROOT, F_SHARED, F_STANDARDIZE, F_CLIP, F_F32L2 = 1, 2, 4, 8, 16, 32
 ACT_ID = {"relu": 0, "tanh": 1, "gelu": 2, "elu": 3}
 WITHIN_ID = {"uniform": 0, "triangular": 1, "gaussian": 2}
 MODE_MCM, MODE_WEIGHTED, MODE_SAMPLE = 0, 1, 2
 STEP_INTS = 32
 (S_KIND, S_ROLE, S_FLAGS, S_ACT, S_NIN, S_INOFF, S_OUTCOL, S_OUTDIM, S_FIXEDCOL, S_K, S_NOUT,
  S_NODEID, S_NOISE, S_AUX0, S_AUX1, S_AUX2, S_OFF_STD, S_OFF_W1, S_OFF_W2, S_OFF_B2, S_OFF_W3,
- S_OFF_B3, S_OFF_TAIL, S_OFF_PTS) = range(24)
+ S_OFF_B3, S_OFF_TAIL, S_OFF_PTS, S_OFF_W2H) = range(25)
 KDE_CHUNKS = 16
 MLP_HIDDEN = (32, 32)
 KDE_MAX_DIMS = 4
@@ -100,6 +100,19 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     for s in range(16):
         w2f[s] = w2[lane & 31, _ROWS[lane >> 5, s]]
     offs["w2"] = blob.add(w2f.reshape(4, 4, 64).transpose(0, 2, 1))            # [4, 64, 4]
+    # split-f16 fragments of v_mfma_f32_32x32x16_f16: k-step s, lane l, element j ->
+    # W2[l&31][16s + 8(j>>2) + 4(l>>5) + (j&3)]; hi = f16(w), lo = f16(w - hi)
+    if np.abs(w2).max() > 32768.0:
+        raise NotImplementedError(f"{rec.kind}: |W2| exceeds the f16 split range")
+    j = np.arange(8)
+    frag = np.zeros((2, 64, 8), np.float32)
+    for s in range(2):
+        for ln in range(64):
+            frag[s, ln] = w2[ln & 31, 16 * s + 8 * (j >> 2) + 4 * (ln >> 5) + (j & 3)]
+    hi = frag.astype(np.float16)
+    lo = (frag - hi.astype(np.float32)).astype(np.float16)
+    halfs = np.concatenate([hi, lo]).reshape(-1)                                # [4, 64, 8] f16
+    offs["w2h"] = blob.add(halfs.view(np.float32))
     offs["b2"] = blob.add(np.concatenate([b2[_ROWS[0]], b2[_ROWS[1]]]))        # [32]
     offs["w3"] = blob.add(np.concatenate([w3[:, _ROWS[0]], w3[:, _ROWS[1]]], axis=1))  # [n_out, 32]
     offs["b3"] = blob.add(b3)
@@ -283,12 +296,13 @@ def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
 
 def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[str],
                logp: Sequence[str], out_nodes: Sequence[str], shared_roots: bool, mode: int,
-               skip: Sequence[str] = ()) -> QueryPlan:
+               skip: Sequence[str] = (), exact_f32: bool = False) -> QueryPlan:
     """Step table for one query signature.
 
     ``latent``: nodes sampled; ``fixed``: nodes read from the fixed buffer (evidence/do);
     ``logp``: nodes whose log p(value | parents) is accumulated; ``out_nodes``: nodes whose
-    values are written per particle; ``skip``: nodes not walked at all.
+    values are written per particle; ``skip``: nodes not walked at all; ``exact_f32``: run
+    the MLPs' hidden layer on the exact f32 MFMA chain instead of the split-f16 product.
     """
     model = packed.model
     latent_s, fixed_s, logp_s, skip_s = set(latent), set(fixed), set(logp), set(skip)
@@ -357,6 +371,8 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
             fl |= F_LOGP
         if shared_roots and (npk.flags & F_ROOT):
             fl |= F_SHARED
+        if exact_f32:
+            fl |= F_F32L2
         row[S_FLAGS] = fl
         row[S_ACT] = npk.act
         row[S_NIN] = npk.n_in
@@ -374,7 +390,8 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         row[S_AUX0] = npk.aux0
         row[S_AUX1] = npk.aux1
         for key, idx in (("std", S_OFF_STD), ("w1", S_OFF_W1), ("w2", S_OFF_W2), ("b2", S_OFF_B2),
-                         ("w3", S_OFF_W3), ("b3", S_OFF_B3), ("tail", S_OFF_TAIL), ("pts", S_OFF_PTS)):
+                         ("w3", S_OFF_W3), ("b3", S_OFF_B3), ("tail", S_OFF_TAIL), ("pts", S_OFF_PTS),
+                         ("w2h", S_OFF_W2H)):
             row[idx] = npk.offs.get(key, 0)
     out_cols: List[int] = []
     for n in out_nodes:
