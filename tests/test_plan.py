@@ -13,7 +13,7 @@ from conftest import golden_names, load_golden
 from vectorizedbayesiannetwork_amd import synthetic
 from vectorizedbayesiannetwork_amd.model import model_from_checkpoint, random_init_model
 from vectorizedbayesiannetwork_amd.plan import (F_LOGP, MODE_MCM, MODE_WEIGHTED, ROLE_FIXED, ROLE_LATENT,
-                                                S_INOFF, S_NIN, S_OFF_B2, S_OFF_B3, S_OFF_STD, S_OFF_W1,
+                                                S_INOFF, S_NIN, S_OFF_B2, S_OFF_B3, S_OFF_W2H, S_OFF_STD, S_OFF_W1,
                                                 S_OFF_W2, S_OFF_W3, S_OUTCOL, S_OUTDIM, S_ROLE, S_FLAGS,
                                                 PackedModel, build_plan)
 
@@ -42,15 +42,45 @@ def permlane32_swap(vdst, vsrc):
     return a, b
 
 
-def emulate_mlp(P, row, parents64, std):
+def mfma_32x32x16_split(P, row, hb, lanes):
+    """Layer 2 as the kernel's split-f16 product: A/B lane l, element j <-> k = 8(l>>5) + j of
+    the K=16 step; B from the layer-1 accumulator registers 8s + j (hi by masking the low 13
+    mantissa bits, lo = x - hi rounded to f16); accumulator starts from the packed b2."""
+    halfs = P.astype(np.float32)[row[S_OFF_W2H]: row[S_OFF_W2H] + 4 * 64 * 4].view(np.float16)
+    frag = halfs.reshape(4, 64, 8).astype(np.float64)          # hi s0, hi s1, lo s0, lo s1
+    d = acc_init(P, row, 1)
+    for s in range(2):
+        A = np.zeros((32, 16)); Bh = np.zeros((16, 32)); Bl = np.zeros((16, 32)); Al = np.zeros((32, 16))
+        for l in range(64):
+            h = l >> 5
+            x = hb[l, 8 * s: 8 * s + 8].astype(np.float32)
+            hi = (x.view(np.int32) & np.int32(-8192)).view(np.float32)
+            Bh[8 * h: 8 * h + 8, l & 31] = hi.astype(np.float16)
+            Bl[8 * h: 8 * h + 8, l & 31] = (x - hi).astype(np.float16)
+            A[l & 31, 8 * h: 8 * h + 8] = frag[s, l]
+            Al[l & 31, 8 * h: 8 * h + 8] = frag[2 + s, l]
+        D = Al @ Bh + A @ Bl + A @ Bh
+        for l in range(64):
+            for r in range(16):
+                d[l, r] += D[_row(r, l >> 5), l & 31]
+    return d
+
+
+def acc_init(P, row, layer):
+    """[64, 16] accumulator initial values: lane l, register r <- b[row(r, l >> 5)]."""
+    b = P[row[S_OFF_B2] + 32 * layer: row[S_OFF_B2] + 32 * layer + 32].reshape(2, 16)
+    return b[np.arange(64) >> 5].astype(np.float64)
+
+
+def emulate_mlp(P, row, parents64, std, split=False):
     """parents64: [nin, 64] values of the 64 particles of a wave -> head [n_out, 64]."""
     nin = row[S_NIN]
-    t1 = (nin + 2) // 2
+    t1 = (nin + 1) // 2
     lanes = np.arange(64)
     half, c = lanes >> 5, lanes & 31
     h2 = []
     for g in range(2):
-        acc = np.zeros((64, 16))
+        acc = acc_init(P, row, 0)
         for t in range(t1):
             kk = 2 * t + half
             z = np.zeros(64)
@@ -60,21 +90,21 @@ def emulate_mlp(P, row, parents64, std):
                     if std:
                         v = (v - P[row[S_OFF_STD] + kk[l]]) * P[row[S_OFF_STD] + nin + kk[l]]
                     z[l] = v
-                elif kk[l] == nin:
-                    z[l] = 1.0
             acc = mfma_32x32x2(P[row[S_OFF_W1] + t * 64: row[S_OFF_W1] + t * 64 + 64], z, acc)
         hb = np.maximum(acc, 0)
-        w2 = P[row[S_OFF_W2]: row[S_OFF_W2] + 1024].reshape(4, 64, 4)
-        b = np.zeros((64, 16))
-        for s in range(16):
-            b = mfma_32x32x2(w2[s // 4, :, s % 4], hb[:, s], b)
+        if split:
+            b = mfma_32x32x16_split(P, row, hb, lanes)
+        else:
+            w2 = P[row[S_OFF_W2]: row[S_OFF_W2] + 1024].reshape(4, 64, 4)
+            b = acc_init(P, row, 1)
+            for s in range(16):
+                b = mfma_32x32x2(w2[s // 4, :, s % 4], hb[:, s], b)
         h2.append(b)
-    b2 = P[row[S_OFF_B2]: row[S_OFF_B2] + 32]
     X = np.zeros((64, 16)); Y = np.zeros((64, 16))
     for r in range(16):
         x, y = permlane32_swap(h2[0][:, r], h2[1][:, r])
-        X[:, r] = np.maximum(x + b2[r], 0)
-        Y[:, r] = np.maximum(y + b2[16 + r], 0)
+        X[:, r] = np.maximum(x, 0)
+        Y[:, r] = np.maximum(y, 0)
     n_out = row[10]
     w3 = P[row[S_OFF_W3]: row[S_OFF_W3] + 32 * n_out].reshape(n_out, 32)
     b3 = P[row[S_OFF_B3]: row[S_OFF_B3] + n_out]
@@ -99,6 +129,7 @@ def test_mfma_fragment_packing_reproduces_torch_mlp(name):
         parents64 = rng.normal(size=(rec.input_dim, 64))
         std = rec.kind == "gaussian_nn"
         got = emulate_mlp(P, row, parents64, std)
+        got_split = emulate_mlp(P, row, parents64, std, split=True)
         x = torch.tensor(parents64.T, dtype=torch.float64)
         if std:
             x = (x - rec.state["mean_x"].double()) / rec.state["std_x"].double()
@@ -109,6 +140,7 @@ def test_mfma_fragment_packing_reproduces_torch_mlp(name):
             if i + 1 < len(layers):
                 h = torch.relu(h)
         np.testing.assert_allclose(got, h.numpy().T, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(got_split, h.numpy().T, rtol=2e-5, atol=2e-5)
         checked += 1
     assert checked > 0
 

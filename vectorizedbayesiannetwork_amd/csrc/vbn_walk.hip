@@ -35,6 +35,8 @@
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // step field holding the split-f16 W2 fragments (vbn_step.reserved[0])
 #define OFF_W2H(st) ((st).reserved[0])
@@ -75,16 +77,14 @@ __device__ __forceinline__ float softplus_t(float x) {
   return __logf(u) * __fdividef(e, u - 1.0f);
 }
 
-// Philox-4x32-10 counter-based RNG.
-__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+// Philox-2x32-10 counter-based RNG (Random123): counter (c0, c1), 32-bit key; one
+// v_mad_u64_u32 per round.
+__device__ __forceinline__ uint2 philox2x32(uint2 c, uint32_t k) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;   // one v_mad_u64_u32 per product
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
-    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k.x, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k.y,
-                   (uint32_t)p0);
-    k.x += 0x9E3779B9u;
-    k.y += 0xBB67AE85u;
+    const uint64_t p = (uint64_t)0xD256D193u * c.x;
+    c = make_uint2((uint32_t)(p >> 32) ^ k ^ c.y, (uint32_t)p);
+    k += 0x9E3779B9u;
   }
   return c;
 }
@@ -98,12 +98,6 @@ __device__ __forceinline__ float box_muller(uint32_t a, uint32_t b) {
   return r * __builtin_amdgcn_cosf(u2);                              // cos(2*pi*u2)
 }
 
-struct Draw {
-  float ucat;  // uniform for a categorical / index choice (slot 0)
-  float z;     // standard normal (slot 1)
-  float u;     // uniform (slot 1)
-};
-
 struct Lane {
   const float* P;        // parameter blob (from a __restrict__ kernel argument)
   const int32_t* ic;     // parent column slots (from a __restrict__ kernel argument)
@@ -115,28 +109,37 @@ struct Lane {
   int s;         // sample
 };
 
-__device__ __forceinline__ Draw get_draw(const vbn_walk_args& A, const vbn_step& st, int d,
-                                         const Lane& L) {
-  Draw r;
-  if (A.noise) {
-    const int64_t bq = A.noise_b == 1 ? 0 : L.b;
-    const int64_t stride_slot = (int64_t)A.noise_b * A.n_samples * A.dmax;
-    const int64_t base = ((int64_t)st.noise_idx * 2) * stride_slot +
-                         (bq * A.n_samples + L.s) * A.dmax + d;
-    r.ucat = A.noise[base];
-    r.z = A.noise[base + stride_slot];
-    r.u = r.z;
-    return r;
-  }
+// Draws of node ``st``, dimension d, for this particle.  Stream 0 gives a standard normal
+// (Box-Muller on both words), stream 1 two uniforms: the categorical / index choice and the
+// within-bin uniform.  Counter = (sample, query ^ seed_hi), key = seed_lo + stream id, where
+// the query key is 0 for draws shared by all queries (root nodes in MCM/LW/ancestral, Q5).
+// With injected noise (parity tests) slot 0 = categorical uniform, slot 1 = normal / uniform.
+__device__ __forceinline__ uint2 rng_words(const vbn_walk_args& A, const vbn_step& st, int d, int stream,
+                                           const Lane& L) {
   const uint32_t qkey = (st.flags & VBN_F_SHARED) ? 0u : (uint32_t)(A.q_base + L.b + 1);
-  const uint4 c = make_uint4((uint32_t)L.s, qkey, (uint32_t)(st.node_id * 16 + d),
-                             (uint32_t)A.offset);
-  const uint2 k = make_uint2((uint32_t)A.seed, (uint32_t)(A.seed >> 32) ^ (uint32_t)(A.offset >> 32));
-  const uint4 x = philox4x32(c, k);
-  r.ucat = u01(x.x);
-  r.z = box_muller(x.y, x.z);
-  r.u = u01(x.w);
-  return r;
+  const uint32_t sid = ((uint32_t)(A.offset & 0xffu) << 24) |
+                       (((uint32_t)st.node_id * 16u + (uint32_t)d) * 2u + (uint32_t)stream);
+  return philox2x32(make_uint2((uint32_t)L.s, qkey ^ (uint32_t)(A.seed >> 32)), (uint32_t)A.seed + sid);
+}
+
+__device__ __forceinline__ int64_t noise_index(const vbn_walk_args& A, const vbn_step& st, int d, int slot,
+                                               const Lane& L) {
+  const int64_t bq = A.noise_b == 1 ? 0 : L.b;
+  const int64_t stride_slot = (int64_t)A.noise_b * A.n_samples * A.dmax;
+  return ((int64_t)st.noise_idx * 2 + slot) * stride_slot + (bq * A.n_samples + L.s) * A.dmax + d;
+}
+
+__device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
+  if (A.noise) return A.noise[noise_index(A, st, d, 1, L)];
+  const uint2 w = rng_words(A, st, d, 0, L);
+  return box_muller(w.x, w.y);
+}
+
+// (categorical uniform, within-bin uniform)
+__device__ __forceinline__ float2 draw_uniforms(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
+  if (A.noise) return make_float2(A.noise[noise_index(A, st, d, 0, L)], A.noise[noise_index(A, st, d, 1, L)]);
+  const uint2 w = rng_words(A, st, d, 1, L);
+  return make_float2(u01(w.x), u01(w.y));
 }
 
 __device__ __forceinline__ float vread(const Lane& L, int slot) { return L.vals[slot * WAVE + L.lane]; }
@@ -152,9 +155,9 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
 // MLP (in -> 32 -> 32 -> n_out) for the wave's 64 particles; head outputs to scr[j][lane].
 //
 // Two 32-particle groups per wave (g = 0: particles 0-31, g = 1: 32-63).  Both hidden layers
-// run on v_mfma_f32_32x32x2_f32 with the hidden unit on M and the particle on N; b1 rides
-// as an extra K column fed a constant 1 (free for odd n_in), so no accumulator is initialised.
-//   layer 1: K = n_in + 1 (z, 1),  A = W1aug fragments, B = z of the lane's particle
+// run with the hidden unit on M and the particle on N; both accumulators start from the layer's
+// bias (register r of lane half h = b[row(r, h)], four 16-byte loads, exact f32).
+//   layer 1: K = n_in on v_mfma_f32_32x32x2_f32, A = W1 fragments, B = z of the lane's particle
 //   layer 2: K = 32 on v_mfma_f32_32x32x16_f16 as a 3-pass split product: x = hi + lo with
 //            hi = f16(x), lo = f16(x - hi) for both operands; A_lo.B_hi + A_hi.B_lo + A_hi.B_hi
 //            accumulated in f32 (relative error ~2^-22 per product, i.e. fp32-level) at 1/5
@@ -162,24 +165,23 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
 //            of lane half h holds hidden row 16s + 8(j>>2) + 4h + (j&3), and the host packs
 //            W2 in that k order.  If any |h| > 32768 (f16 range) the wave takes the exact
 //            f32 chain (v_mfma_f32_32x32x2_f32, k-step s pairs rows (row(s,0), row(s,1))).
-//            b2 is added after the transpose (SGPRs).
 //   head   : 16 v_permlane32_swap transpose the layer-2 accumulators so lane l holds all 32
 //            hidden units of particle l; the head then runs on VALU with wave-uniform weights.
 //
 // Parameter blocks (packed by vectorizedbayesiannetwork_amd/plan.py):
 //   off_std : mean_x[n_in], 1/std_x[n_in]                            (gaussian_nn only)
-//   off_w1  : [t][64]  lane l: W1aug[l&31][2t + (l>>5)],  W1aug = [W1 | b1 | 0]
-//   off_w2  : [q 4][lane 64][4], step s = 4q+e: W2[l&31][row(s, l>>5)]   (f32 fallback)
+//   off_w1  : [t][64]  lane l: W1z[l&31][2t + (l>>5)],  W1z = [W1 | 0] (even width)
+//   off_b2  : [layer 2][half 2][16] = b1[row(r, h)], then b2[row(r, h)]  (accumulator init)
+//   off_w2  : [q 4][lane 64][4], step s = 4q+e: W2[l&31][row(s, l>>5)]   (exact f32 fallback)
 //   off_w2h : [4][lane 64][8 f16]: hi(s=0), hi(s=1), lo(s=0), lo(s=1);
 //             element j of lane l: W2[l&31][16s + 8(j>>2) + 4(l>>5) + (j&3)]
-//   off_b2  : [32] = b2[row(r,0)] (r<16) ++ b2[row(r,1)]
 //   off_w3  : [n_out][32] = W3[j][row(r,0)] (r<16) ++ W3[j][row(r,1)]
 //   off_b3  : [n_out]
 // with row(r, h) = (r&3) + 8(r>>2) + 4h, the 32x32 accumulator row of register r, half h.
 // ------------------------------------------------------------------------------------------
 
 // layer-1 B operand of k-step t for group g: z[2t + half] of particle (c + 32 g); the
-// bias column n_in is the constant 1, columns beyond it are 0.
+// column beyond n_in (odd n_in) is 0.
 template <bool STD, int NIN>
 __device__ __forceinline__ float l1_operand(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
                                             int t, int g) {
@@ -195,7 +197,7 @@ __device__ __forceinline__ float l1_operand(const vbn_walk_args& A, const vbn_st
     const float is = half ? P[st.off_std + nin + ko] : P[st.off_std + nin + ke];
     z = (z - m) * is;
   }
-  return kk < nin ? z : (kk == nin ? 1.0f : 0.0f);
+  return kk < nin ? z : 0.0f;
 }
 
 template <int ACT, bool STD, int NIN>
@@ -203,7 +205,7 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
   const float* __restrict__ P = L.P;
   const int lane = L.lane;
   const int nin = NIN > 0 ? NIN : st.n_in;
-  const int t1 = (nin + 2) >> 1;                  // layer-1 k-steps incl. the bias column
+  const int t1 = (nin + 1) >> 1;                  // layer-1 k-steps
 
   bool nan_in = false;                            // torch keeps NaN through Linear/act
   for (int d = 0; d < nin; ++d) {
@@ -213,22 +215,22 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
 
   // layer-2 A fragments, split f16 (hi, lo) for the two K=16 steps (see header)
   const uint4* w2h = reinterpret_cast<const uint4*>(P + OFF_W2H(st));
-  f16x8 ah[2], al[2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    ah[s2] = __builtin_bit_cast(f16x8, w2h[s2 * WAVE + lane]);
-    al[s2] = __builtin_bit_cast(f16x8, w2h[(2 + s2) * WAVE + lane]);
-  }
+  const float4* bacc = reinterpret_cast<const float4*>(P + st.off_b2 + 16 * (lane >> 5));
 
   f16x8 bh[2], bl[2];
   f32x16 h2[2];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
-    // layer 1 (+ bias column)
-    f32x16 a = {};
+    // layer 1, accumulator initialised with b1
+    f32x16 a;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = bacc[q];
+      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
+    }
     if (NIN > 0) {
 #pragma unroll
-      for (int t = 0; t < (NIN + 2) / 2; ++t)
+      for (int t = 0; t < (NIN + 1) / 2; ++t)
         a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
                                                  l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
     } else {
@@ -243,25 +245,38 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
       hb[r] = act_fn<ACT>(a[r]);
       big = max(big, (unsigned)__float_as_int(hb[r]) & 0x7fffffffu);   // |h| as ordered bits; NaN counts as big
     }
-    f32x16 b = {};
+    f32x16 b;                                     // layer 2, initialised with b2
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = bacc[8 + q];
+      b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+    }
     if (!(st.flags & VBN_F_F32L2) && !__any(big > 0x47000000u)) {  // |h| <= 32768: in f16 split range
       // layer 2 as three f16 MFMAs per K=16 step: A_lo.B_hi + A_hi.B_lo + A_hi.B_hi (f32 accumulate).
       // B operand: register 8s+j of lane half h holds hidden row 16s + 8(j>>2) + 4h + (j&3).
+      // hi = x with the low 13 mantissa bits cleared (exactly an f16 in range), lo = x - hi (exact)
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = hb[8 * s2 + j];
-          const _Float16 hi = (_Float16)x;
-          bh[s2][j] = hi;
-          bl[s2][j] = (_Float16)(x - (float)hi);
+        for (int j = 0; j < 8; j += 2) {
+          const float x0 = hb[8 * s2 + j], x1 = hb[8 * s2 + j + 1];
+          const float h0 = __int_as_float(__float_as_int(x0) & 0xFFFFE000);
+          const float h1 = __int_as_float(__float_as_int(x1) & 0xFFFFE000);
+          const f16x2 ph = __builtin_convertvector((f32x2){h0, h1}, f16x2);
+          const f16x2 pl = __builtin_convertvector((f32x2){x0 - h0, x1 - h1}, f16x2);
+          bh[s2][j] = ph[0];
+          bh[s2][j + 1] = ph[1];
+          bl[s2][j] = pl[0];
+          bl[s2][j + 1] = pl[1];
         }
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[s2], bh[s2], b, 0, 0, 0);
-        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2], bl[s2], b, 0, 0, 0);
-        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[s2], bh[s2], b, 0, 0, 0);
+        const f16x8 ah = __builtin_bit_cast(f16x8, w2h[s2 * WAVE + lane]);   // re-read per group (L1)
+        const f16x8 al = __builtin_bit_cast(f16x8, w2h[(2 + s2) * WAVE + lane]);
+        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s2], b, 0, 0, 0);
+        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s2], b, 0, 0, 0);
+        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s2], b, 0, 0, 0);
       }
     } else {
       // exact f32 chain (K = 32 as 16 steps of 2), W2 fragments in off_w2
@@ -278,14 +293,13 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
     h2[g] = b;
   }
 
-  // transpose: lane l <- all 32 hidden units of particle l; + b2 (wave-uniform), activation
-  const float* __restrict__ b2 = P + st.off_b2;    // [32] = b2[row(r,0)] ++ b2[row(r,1)]
+  // transpose: lane l <- all 32 hidden units of particle l (b2 already in), activation
   float X[16], Y[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(h2[0][r]), __float_as_uint(h2[1][r]), false, false);
-    X[r] = act_fn<ACT>(__uint_as_float(sw[0]) + b2[r]);        // hidden row(r, 0)
-    Y[r] = act_fn<ACT>(__uint_as_float(sw[1]) + b2[16 + r]);   // hidden row(r, 1)
+    X[r] = act_fn<ACT>(__uint_as_float(sw[0]));   // hidden row(r, 0)
+    Y[r] = act_fn<ACT>(__uint_as_float(sw[1]));   // hidden row(r, 1)
   }
 
   // head (wave-uniform weights)
@@ -354,8 +368,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
       const float loc = t[d], scale = t[D + d];
       float x;
       if (latent) {
-        const Draw r = get_draw(A, st, d, L);
-        x = r.z * scale + loc;                       // torch.normal(loc, scale)
+        x = draw_normal(A, st, d, L) * scale + loc;  // torch.normal(loc, scale)
         vwrite(L, st.out_col + d, x);
       } else {
         x = fixed_value(A, st, d, L);
@@ -379,8 +392,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
     const float scale = (softplus_t(o_sc) + min_scale) * sy;
     float x;
     if (latent) {
-      const Draw r = get_draw(A, st, d, L);
-      x = loc + r.z * scale;
+      x = loc + draw_normal(A, st, d, L) * scale;
     } else {
       x = fixed_value(A, st, d, L);
     }
@@ -414,8 +426,7 @@ __device__ __forceinline__ void step_linear_gaussian(const vbn_walk_args& A, con
     const float loc = (nin > 0) ? mu + bias[d] : bias[d];
     float x;
     if (latent) {
-      const Draw r = get_draw(A, st, d, L);
-      x = loc + r.z * scale[d];
+      x = loc + draw_normal(A, st, d, L) * scale[d];
     } else {
       x = fixed_value(A, st, d, L);
     }
@@ -486,12 +497,9 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
                 : softplus_t(scr[(K + k * 2 * D + D + d) * WAVE + lane]) + min_scale;
   };
   if (latent) {
-    const Draw r0 = get_draw(A, st, 0, L);
-    const int idx = inv_cdf(K, r0.ucat, pi_k);
-    for (int d = 0; d < D; ++d) {
-      const Draw r = d == 0 ? r0 : get_draw(A, st, d, L);
-      vwrite(L, st.out_col + d, loc_kd(idx, d) + r.z * scale_kd(idx, d));
-    }
+    const int idx = inv_cdf(K, draw_uniforms(A, st, 0, L).x, pi_k);
+    for (int d = 0; d < D; ++d)
+      vwrite(L, st.out_col + d, loc_kd(idx, d) + draw_normal(A, st, d, L) * scale_kd(idx, d));
   } else {
     for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
   }
@@ -565,8 +573,8 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
     float x;
     int idx;
     if (latent) {
-      const Draw r = get_draw(A, st, d, L);
-      idx = inv_cdf(C, r.ucat, [&](int c) { return __expf(logit(c) - m) / se; });
+      const float2 uu = draw_uniforms(A, st, d, L);
+      idx = inv_cdf(C, uu.x, [&](int c) { return __expf(logit(c) - m) / se; });
       const float left = e[idx];
       const float right = e[idx + 1 < C ? idx + 1 : C];
       const float width = fmaxf(right - left, min_bw);
@@ -576,13 +584,13 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
       } else {
         float cont;
         if (mode == VBN_WITHIN_UNIFORM) {
-          cont = left + r.u * width;
+          cont = left + uu.y * width;
         } else if (mode == VBN_WITHIN_TRIANGULAR) {
-          const float lv = left + width * sqrtf(fmaxf(r.u * 0.5f, 0.0f));
-          const float rv = right - width * sqrtf(fmaxf((1.0f - r.u) * 0.5f, 0.0f));
-          cont = r.u < 0.5f ? lv : rv;
+          const float lv = left + width * sqrtf(fmaxf(uu.y * 0.5f, 0.0f));
+          const float rv = right - width * sqrtf(fmaxf((1.0f - uu.y) * 0.5f, 0.0f));
+          cont = uu.y < 0.5f ? lv : rv;
         } else {
-          cont = center + r.z * fmaxf(wscale * width, min_bw);
+          cont = center + draw_normal(A, st, d, L) * fmaxf(wscale * width, min_bw);
         }
         if (clip) cont = fminf(fmaxf(cont, left), right);
         x = cont;
@@ -692,10 +700,10 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
   for (int i = 0; i < (DP > 0 ? DP : 0); ++i) pv[i] = vread(L, L.ic[st.in_off + i]);
 
   if (st.role == VBN_ROLE_LATENT) {
-    const Draw r0 = get_draw(A, st, 0, L);
+    const float ucat = draw_uniforms(A, st, 0, L).x;
     int idx;
     if (root) {
-      idx = min((int)(r0.ucat * (float)M), M - 1);          // randint(0, M)
+      idx = min((int)(ucat * (float)M), M - 1);             // randint(0, M)
     } else {
       // pass 1: per-chunk weight sums -> scr[chunk][lane]
       const int csz = (M + KDE_CHUNKS - 1) / KDE_CHUNKS;
@@ -726,7 +734,7 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
         }
       }
       // pass 2: locate the chunk, then scan inside it (per-lane chunk; vector loads)
-      const double thr = (double)r0.ucat * tot;
+      const double thr = (double)ucat * tot;
       double cum = 0.0;
       int ch = KDE_CHUNKS - 1;
       for (int c2 = 0; c2 < KDE_CHUNKS; ++c2) {
@@ -745,9 +753,8 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
       wave_sync();
     }
     for (int d = 0; d < D; ++d) {
-      const Draw r = d == 0 ? r0 : get_draw(A, st, d, L);
       const float sel = pts[(int64_t)idx * stride + dp + d];
-      vwrite(L, st.out_col + d, sel + r.z * noise_scale);
+      vwrite(L, st.out_col + d, sel + draw_normal(A, st, d, L) * noise_scale);
     }
   } else {
     for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
@@ -818,7 +825,7 @@ __device__ __forceinline__ void step_kde(const vbn_walk_args& A, const vbn_step&
 // bit5 non-relu activations.  Each instantiation only carries the code (and registers) of
 // the CPD kinds a plan uses.
 template <unsigned KM>
-__global__ void __launch_bounds__(WAVE) vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params,
+__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params,
                                                         const vbn_step* __restrict__ steps,
                                                         const int32_t* __restrict__ in_cols) {
   extern __shared__ __attribute__((aligned(16))) float smem[];

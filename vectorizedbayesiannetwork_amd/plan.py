@@ -74,7 +74,7 @@ def _np(t: torch.Tensor) -> np.ndarray:
 
 
 def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
-    """MFMA fragment layouts of csrc/vbn_walk.hip mlp_forward (biases as constant-1 K columns)."""
+    """MFMA fragment layouts of csrc/vbn_walk.hip mlp_forward (biases as accumulator init)."""
     layers = rec.mlp_layers()
     hidden = tuple(int(w.shape[0]) for w, _ in layers[:-1])
     if hidden != MLP_HIDDEN:
@@ -89,17 +89,18 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
         offs["std"] = blob.add(np.concatenate([_np(rec.state["mean_x"]), inv]))
     else:
         offs["std"] = 0
-    t1 = (nin + 2) // 2
-    w1aug = np.zeros((32, 2 * t1), np.float32)
-    w1aug[:, :nin] = w1
-    w1aug[:, nin] = b1
+    t1 = (nin + 1) // 2
+    w1z = np.zeros((32, 2 * t1), np.float32)
+    w1z[:, :nin] = w1
     lane = np.arange(64)
-    w1f = np.stack([w1aug[lane & 31, 2 * t + (lane >> 5)] for t in range(t1)])   # [t1, 64]
+    w1f = np.stack([w1z[lane & 31, 2 * t + (lane >> 5)] for t in range(t1)])   # [t1, 64]
     offs["w1"] = blob.add(w1f)
+    # accumulator init: [layer][half h][register r] = b[row(r, h)]
+    offs["b2"] = blob.add(np.stack([b1[_ROWS[:, :16]], b2[_ROWS[:, :16]]]))    # [2, 2, 16]
     w2f = np.zeros((16, 64), np.float32)
     for s in range(16):
         w2f[s] = w2[lane & 31, _ROWS[lane >> 5, s]]
-    offs["w2"] = blob.add(w2f.reshape(4, 4, 64).transpose(0, 2, 1))            # [4, 64, 4]
+    offs["w2"] = blob.add(w2f.reshape(4, 4, 64).transpose(0, 2, 1))            # [4, 64, 4] (exact f32)
     # split-f16 fragments of v_mfma_f32_32x32x16_f16: k-step s, lane l, element j ->
     # W2[l&31][16s + 8(j>>2) + 4(l>>5) + (j&3)]; hi = f16(w), lo = f16(w - hi)
     if np.abs(w2).max() > 32768.0:
@@ -111,9 +112,8 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
             frag[s, ln] = w2[ln & 31, 16 * s + 8 * (j >> 2) + 4 * (ln >> 5) + (j & 3)]
     hi = frag.astype(np.float16)
     lo = (frag - hi.astype(np.float32)).astype(np.float16)
-    halfs = np.concatenate([hi, lo]).reshape(-1)                                # [4, 64, 8] f16
+    halfs = np.concatenate([hi, lo]).reshape(-1)                               # [4, 64, 8] f16
     offs["w2h"] = blob.add(halfs.view(np.float32))
-    offs["b2"] = blob.add(np.concatenate([b2[_ROWS[0]], b2[_ROWS[1]]]))        # [32]
     offs["w3"] = blob.add(np.concatenate([w3[:, _ROWS[0]], w3[:, _ROWS[1]]], axis=1))  # [n_out, 32]
     offs["b3"] = blob.add(b3)
     offs["n_out"] = w3.shape[0]
