@@ -68,7 +68,7 @@ def mfma_32x32x16_split(P, row, hb, lanes):
 
 def acc_init(P, row, layer):
     """[64, 16] accumulator initial values: lane l, register r <- b[row(r, l >> 5)]."""
-    b = P[row[S_OFF_B2] + 32 * layer: row[S_OFF_B2] + 32 * layer + 32].reshape(2, 16)
+    b = P[row[S_OFF_B2] + 64 * layer: row[S_OFF_B2] + 64 * layer + 32].reshape(2, 16)
     return b[np.arange(64) >> 5].astype(np.float64)
 
 

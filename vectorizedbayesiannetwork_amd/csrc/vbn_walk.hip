@@ -171,7 +171,8 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
 // Parameter blocks (packed by vectorizedbayesiannetwork_amd/plan.py):
 //   off_std : mean_x[n_in], 1/std_x[n_in]                            (gaussian_nn only)
 //   off_w1  : [t][64]  lane l: W1z[l&31][2t + (l>>5)],  W1z = [W1 | 0] (even width)
-//   off_b2  : [layer 2][half 2][16] = b1[row(r, h)], then b2[row(r, h)]  (accumulator init)
+//   off_b2  : [layer 2][group 2][half 2][16] = b[row(r, h)] (accumulator init; the two group
+//             copies are identical)
 //   off_w2  : [q 4][lane 64][4], step s = 4q+e: W2[l&31][row(s, l>>5)]   (exact f32 fallback)
 //   off_w2h : [4][lane 64][8 f16]: hi(s=0), hi(s=1), lo(s=0), lo(s=1);
 //             element j of lane l: W2[l&31][16s + 8(j>>2) + 4(l>>5) + (j&3)]
@@ -200,121 +201,161 @@ __device__ __forceinline__ float l1_operand(const vbn_walk_args& A, const vbn_st
   return kk < nin ? z : 0.0f;
 }
 
-template <int ACT, bool STD, int NIN>
-__device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+// layer-1 accumulator of group g: b1 + W1 z (K = n_in, k-steps of 2)
+template <bool STD, int NIN>
+__device__ __forceinline__ f32x16 mlp_layer1(const vbn_walk_args& A, const vbn_step& st, const Lane& L, int g) {
   const float* __restrict__ P = L.P;
   const int lane = L.lane;
-  const int nin = NIN > 0 ? NIN : st.n_in;
-  const int t1 = (nin + 1) >> 1;                  // layer-1 k-steps
-
-  bool nan_in = false;                            // torch keeps NaN through Linear/act
-  for (int d = 0; d < nin; ++d) {
-    const float v = L.vals[L.ic[st.in_off + d] * WAVE + lane];
-    nan_in |= (v != v);
+  const float4* bacc = reinterpret_cast<const float4*>(P + st.off_b2 + 32 * g + 16 * (lane >> 5));
+  f32x16 a;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = bacc[q];
+    a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
   }
-
-  // layer-2 A fragments, split f16 (hi, lo) for the two K=16 steps (see header)
-  const uint4* w2h = reinterpret_cast<const uint4*>(P + OFF_W2H(st));
-  const float4* bacc = reinterpret_cast<const float4*>(P + st.off_b2 + 16 * (lane >> 5));
-
-  f16x8 bh[2], bl[2];
-  f32x16 h2[2];
+  if (NIN > 0) {
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    // layer 1, accumulator initialised with b1
-    f32x16 a;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v = bacc[q];
-      a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-    }
-    if (NIN > 0) {
-#pragma unroll
-      for (int t = 0; t < (NIN + 1) / 2; ++t)
-        a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
-                                                 l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
-    } else {
-      for (int t = 0; t < t1; ++t)
-        a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
-                                                 l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
-    }
-    float hb[16];
-    unsigned big = 0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      hb[r] = act_fn<ACT>(a[r]);
-      big = max(big, (unsigned)__float_as_int(hb[r]) & 0x7fffffffu);   // |h| as ordered bits; NaN counts as big
-    }
-    f32x16 b;                                     // layer 2, initialised with b2
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v = bacc[8 + q];
-      b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
-    }
-    if (!(st.flags & VBN_F_F32L2) && !__any(big > 0x47000000u)) {  // |h| <= 32768: in f16 split range
-      // layer 2 as three f16 MFMAs per K=16 step: A_lo.B_hi + A_hi.B_lo + A_hi.B_hi (f32 accumulate).
-      // B operand: register 8s+j of lane half h holds hidden row 16s + 8(j>>2) + 4h + (j&3).
-      // hi = x with the low 13 mantissa bits cleared (exactly an f16 in range), lo = x - hi (exact)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const float x0 = hb[8 * s2 + j], x1 = hb[8 * s2 + j + 1];
-          const float h0 = __int_as_float(__float_as_int(x0) & 0xFFFFE000);
-          const float h1 = __int_as_float(__float_as_int(x1) & 0xFFFFE000);
-          const f16x2 ph = __builtin_convertvector((f32x2){h0, h1}, f16x2);
-          const f16x2 pl = __builtin_convertvector((f32x2){x0 - h0, x1 - h1}, f16x2);
-          bh[s2][j] = ph[0];
-          bh[s2][j + 1] = ph[1];
-          bl[s2][j] = pl[0];
-          bl[s2][j + 1] = pl[1];
-        }
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const f16x8 ah = __builtin_bit_cast(f16x8, w2h[s2 * WAVE + lane]);   // re-read per group (L1)
-        const f16x8 al = __builtin_bit_cast(f16x8, w2h[(2 + s2) * WAVE + lane]);
-        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s2], b, 0, 0, 0);
-        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s2], b, 0, 0, 0);
-        b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s2], b, 0, 0, 0);
-      }
-    } else {
-      // exact f32 chain (K = 32 as 16 steps of 2), W2 fragments in off_w2
-      const float4* w2p = reinterpret_cast<const float4*>(P + st.off_w2);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = w2p[q * WAVE + lane];
-        b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, hb[4 * q + 0], b, 0, 0, 0);
-        b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, hb[4 * q + 1], b, 0, 0, 0);
-        b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, hb[4 * q + 2], b, 0, 0, 0);
-        b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, hb[4 * q + 3], b, 0, 0, 0);
-      }
-    }
-    h2[g] = b;
+    for (int t = 0; t < (NIN + 1) / 2; ++t)
+      a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
+                                               l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
+  } else {
+    const int t1 = (st.n_in + 1) >> 1;
+    for (int t = 0; t < t1; ++t)
+      a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
+                                               l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
   }
+  return a;
+}
 
-  // transpose: lane l <- all 32 hidden units of particle l (b2 already in), activation
-  float X[16], Y[16];
+// layer-2 bias as the accumulator's initial value (one copy per group: distinct addresses keep
+// the two groups' loads apart, so each lands directly in its accumulator)
+__device__ __forceinline__ f32x16 layer2_init(const vbn_step& st, const Lane& L, int g) {
+  const float4* bacc = reinterpret_cast<const float4*>(L.P + st.off_b2 + 64 + 32 * g + 16 * (L.lane >> 5));
+  f32x16 b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = bacc[q];
+    b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
+  }
+  return b;
+}
+
+// y - f32(half h of packed f16 pair hp), exact: one v_fma_mix_f32 (reads the f16 in place).
+// Operands are VALU results (activation / cvt), never raw MFMA results, so no MFMA read hazard.
+__device__ __forceinline__ float sub_f16_lo(float y, uint32_t hp) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(y));
+  return r;
+}
+__device__ __forceinline__ float sub_f16_hi(float y, uint32_t hp) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(y));
+  return r;
+}
+
+// Layer 2 of one group on the split-f16 path: y = act(a); y = hi + lo with hi = f16(y),
+// lo = f16(y - hi); A_lo.B_hi + A_hi.B_lo + A_hi.B_hi on v_mfma_f32_32x32x16_f16 (f32
+// accumulate).  B operand: register 8s+j of lane half h holds hidden row 16s + 8(j>>2) +
+// 4h + (j&3).  Returns false (wave-uniform) when some |y| > 32768 (outside the f16 split range).
+template <int ACT>
+__device__ __forceinline__ bool layer2_split(const vbn_step& st, const Lane& L, int g, const f32x16& a, f32x16& out) {
+  float y[16];
+  int big = 0;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(h2[0][r]), __float_as_uint(h2[1][r]), false, false);
-    X[r] = act_fn<ACT>(__uint_as_float(sw[0]));   // hidden row(r, 0)
-    Y[r] = act_fn<ACT>(__uint_as_float(sw[1]));   // hidden row(r, 1)
+    y[r] = act_fn<ACT>(a[r]);
+    big = max(big, __float_as_int(y[r]));        // activations are >= -1: only the positive side
   }
+  if (__any(big > 0x47000000)) return false;     // (NaN with the sign bit clear counts as big)
+  f16x8 bh[2], bl[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const float y0 = y[8 * s2 + j], y1 = y[8 * s2 + j + 1];
+      const f16x2 ph = __builtin_convertvector((f32x2){y0, y1}, f16x2);
+      const uint32_t hp = __builtin_bit_cast(uint32_t, ph);
+      const f16x2 pl = __builtin_convertvector((f32x2){sub_f16_lo(y0, hp), sub_f16_hi(y1, hp)}, f16x2);
+      bh[s2][j] = ph[0];
+      bh[s2][j + 1] = ph[1];
+      bl[s2][j] = pl[0];
+      bl[s2][j + 1] = pl[1];
+    }
+  }
+  const uint4* w2h = reinterpret_cast<const uint4*>(L.P + OFF_W2H(st));
+  f32x16 b = layer2_init(st, L, g);
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const f16x8 ah = __builtin_bit_cast(f16x8, w2h[s2 * WAVE + L.lane]);
+    const f16x8 al = __builtin_bit_cast(f16x8, w2h[(2 + s2) * WAVE + L.lane]);
+    b = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s2], b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s2], b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s2], b, 0, 0, 0);
+  }
+  out = b;
+  return true;
+}
 
-  // head (wave-uniform weights)
+// Layer 2 of one group, exact f32 chain (K = 32 as 16 v_mfma_f32_32x32x2_f32 steps)
+template <int ACT>
+__device__ __forceinline__ f32x16 layer2_exact(const vbn_step& st, const Lane& L, int g, const f32x16& a) {
+  const float4* w2p = reinterpret_cast<const float4*>(L.P + st.off_w2);
+  f32x16 b = layer2_init(st, L, g);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 v = w2p[q * WAVE + L.lane];
+    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, act_fn<ACT>(a[4 * q + 0]), b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, act_fn<ACT>(a[4 * q + 1]), b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, act_fn<ACT>(a[4 * q + 2]), b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, act_fn<ACT>(a[4 * q + 3]), b, 0, 0, 0);
+  }
+  return b;
+}
+
+// transpose (lane l <- all 32 hidden units of particle l), activation, head on VALU with
+// wave-uniform weight pairs (v_pk_fma_f32), outputs to scr[j][lane]
+template <int ACT>
+__device__ __forceinline__ void mlp_head(const vbn_step& st, const Lane& L, const f32x16& h0, const f32x16& h1,
+                                         bool nan_in) {
+  const float* __restrict__ P = L.P;
+  f32x2 X[8], Y[8];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(h0[r]), __float_as_uint(h1[r]), false, false);
+    X[r >> 1][r & 1] = act_fn<ACT>(__uint_as_float(sw[0]));   // hidden row(r, 0)
+    Y[r >> 1][r & 1] = act_fn<ACT>(__uint_as_float(sw[1]));   // hidden row(r, 1)
+  }
   const int nout = st.n_out;
-  const float* __restrict__ w3 = P + st.off_w3;
+  const f32x2* __restrict__ w3 = reinterpret_cast<const f32x2*>(P + st.off_w3);
 #pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
   for (int j = 0; j < nout; ++j) {
-    float o = P[st.off_b3 + j];
+    f32x2 o = {P[st.off_b3 + j], 0.f};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o = fmaf(w3[j * 32 + r], X[r], o);
+    for (int i = 0; i < 8; ++i) o = __builtin_elementwise_fma(w3[j * 16 + i], X[i], o);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o = fmaf(w3[j * 32 + 16 + r], Y[r], o);
-    L.scr[j * WAVE + lane] = nan_in ? __int_as_float(0x7fc00000) : o;
+    for (int i = 0; i < 8; ++i) o = __builtin_elementwise_fma(w3[j * 16 + 8 + i], Y[i], o);
+    L.scr[j * WAVE + L.lane] = nan_in ? __int_as_float(0x7fc00000) : o[0] + o[1];
   }
   wave_sync();
+}
+
+template <int ACT, bool STD, int NIN>
+__device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  const int nin = NIN > 0 ? NIN : st.n_in;
+  bool nan_in = false;                            // torch keeps NaN through Linear/act
+  for (int d = 0; d < nin; ++d) {
+    const float v = L.vals[L.ic[st.in_off + d] * WAVE + L.lane];
+    nan_in |= (v != v);
+  }
+  // split path unless flagged off or some |hidden| leaves the f16 range (wave-uniform); one
+  // shared head after the merge (an early-return shape doubles the live registers)
+  f32x16 h0, h1;
+  if ((st.flags & VBN_F_F32L2) || !(layer2_split<ACT>(st, L, 0, mlp_layer1<STD, NIN>(A, st, L, 0), h0) &&
+                                    layer2_split<ACT>(st, L, 1, mlp_layer1<STD, NIN>(A, st, L, 1), h1))) {
+    h0 = layer2_exact<ACT>(st, L, 0, mlp_layer1<STD, NIN>(A, st, L, 0));
+    h1 = layer2_exact<ACT>(st, L, 1, mlp_layer1<STD, NIN>(A, st, L, 1));
+  }
+  mlp_head<ACT>(st, L, h0, h1, nan_in);
 }
 
 template <int ACT, bool STD>

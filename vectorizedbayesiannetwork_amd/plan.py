@@ -95,8 +95,8 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     lane = np.arange(64)
     w1f = np.stack([w1z[lane & 31, 2 * t + (lane >> 5)] for t in range(t1)])   # [t1, 64]
     offs["w1"] = blob.add(w1f)
-    # accumulator init: [layer][half h][register r] = b[row(r, h)]
-    offs["b2"] = blob.add(np.stack([b1[_ROWS[:, :16]], b2[_ROWS[:, :16]]]))    # [2, 2, 16]
+    # accumulator init: [layer][group g][half h][register r] = b[row(r, h)] (one copy per group)
+    offs["b2"] = blob.add(np.stack([np.stack([b[_ROWS]] * 2) for b in (b1, b2)]))  # [2, 2, 2, 16]
     w2f = np.zeros((16, 64), np.float32)
     for s in range(16):
         w2f[s] = w2[lane & 31, _ROWS[lane >> 5, s]]
