@@ -38,6 +38,9 @@ FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 dense (vector = f32-input MFMA), MI35
 F16_PEAK_TFLOPS = 2516.6     # f16 MFMA dense: 32x32x16 = 32768 FLOP / 32 cyc / SIMD x 1024 SIMD x 2.4 GHz
 SPLIT_PASSES = 3             # split-f16 hidden layer: A_lo.B_hi + A_hi.B_lo + A_hi.B_hi
 HBM_PEAK_GBS = 8000.0
+# v_exp_f32: 8 issue cycles per wave64 instruction per SIMD (MI355X_MICROARCH.md constants)
+# -> 8 exp/clk/SIMD x 1024 SIMDs x 2.4 GHz
+EXP_PEAK_T = 8 * 1024 * 2.4e9 / 1e12
 
 
 def build_workload(cfg_name: str, device: str, rank: int):
@@ -76,18 +79,21 @@ def mlp_flops_per_particle(model, plan):
     return f32, hidden
 
 
-def kde_pairs_per_particle(model, plan) -> float:
-    pairs = 0.0
+def kde_exps_per_particle(model, plan) -> float:
+    """Algorithmic kernel-weight evaluations (one exp each) of one particle in one walk:
+    M for a sampled non-root KDE node (the CDF pass; the chunk rescan is not counted),
+    2M for a non-root log-prob (LSE over K_p and over K_p K_y), M for a root log-prob."""
+    exps = 0.0
     for i in range(plan.n_steps):
         row = plan.steps[i].tolist()
         if row[0] != KIND_ID["kde"] or row[1] == 0:
             continue
-        m = row[9]
-        if row[1] == 1 and not (row[2] & 2):
-            pairs += m * (1 + 1.0 / 16)          # CDF pass + one chunk rescan
+        m, root = row[9], bool(row[2] & 2)
+        if row[1] == 1 and not root:
+            exps += m
         if row[2] & 1:
-            pairs += m                           # log_prob pass
-    return pairs
+            exps += m if root else 2 * m
+    return exps
 
 
 def cpu_baseline(cfg, model, query, n_queries: int, reps: int = 3):
@@ -203,13 +209,18 @@ def main():
     flops = f32_fl + hid_fl
     exact = bool(getattr(vbn._inference, "exact_f32", False))
     hid_peak = FP32_PEAK_TFLOPS if exact else F16_PEAK_TFLOPS / SPLIT_PASSES
-    pairs = kde_pairs_per_particle(model, plan) * B * S
+    exps = kde_exps_per_particle(model, plan) * B * S
     traffic = load_traffic(args.config)
     kern_s = kern_ms * 1e-3
-    if pairs > 0.1 * flops / 64:
-        # KDE: bound by VALU / v_exp issue (~1 exp + ~6 VALU per pair); priced in pairs/s
-        roof = {"bound": "valu", "achieved": round(pairs / kern_s / 1e12, 4), "peak": None, "unit": "Tpair/s",
-                "frac": None, "traffic": traffic, "kernel": "vbn_walk_kernel", "kernel_ms": round(kern_ms, 4)}
+    if exps > 0.1 * flops / 64:
+        # KDE: one exp per (particle, point) kernel weight; distances on MFMA (16x16x4 f32), the
+        # bound is the v_exp_f32 issue rate
+        ach = exps / kern_s / 1e12
+        roof = {"bound": "exp", "achieved": round(ach, 4), "peak": round(EXP_PEAK_T, 2), "unit": "Texp/s",
+                "frac": round(ach / EXP_PEAK_T, 4), "traffic": traffic, "kernel": "vbn_walk_kernel",
+                "kernel_ms": round(kern_ms, 4), "exps_per_launch": exps,
+                "peak_basis": "v_exp_f32 issue: 8 cyc per wave64 per SIMD, 1024 SIMDs, 2.4 GHz",
+                "launches_timed": reps}
     else:
         # blended peak: each FLOP class at the dense peak of the unit that runs it
         t_min = f32_fl / (FP32_PEAK_TFLOPS * 1e12) + hid_fl / (hid_peak * 1e12)

@@ -37,6 +37,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // step field holding the split-f16 W2 fragments (vbn_step.reserved[0])
 #define OFF_W2H(st) ((st).reserved[0])
@@ -726,6 +727,210 @@ __device__ __forceinline__ float kde_qy(const float* __restrict__ pty, float x0,
   return q;
 }
 
+// ---- pairwise kernel weights on MFMA ------------------------------------------------------
+// The kernel weight of particle n and stored point m is exp(-|x_n - y_m|^2 / (2 s^2)) =
+// exp2(-|x'_n - y'_m|^2) with x' = c x, y' = c y, c = sqrt(log2(e) / 2) / s, and
+//   -|x' - y'|^2 = -|x'|^2 + sum_k (2 x'_k) y'_k - |y'|^2,
+// a contraction over K = nf + 1 <= 4 features: one v_mfma_f32_16x16x4_f32 per 16 points x 16
+// particles with A[m][k] = (y'_0 .. y'_{nf-1}, |y'|^2, 0..) (host-packed as [block][k][16],
+// padding points |y'|^2 = 1e30 -> weight 0), B[k][n] = (2x'_0 .. 2x'_{nf-1}, -1, 0..) and the
+// accumulator input C = -|x'_n|^2.  The MFMA is a k-ordered fmaf chain from C, so
+// kde_arg_replica() reproduces any element bit-for-bit on VALU (the inverse-CDF scan).
+// The wave's 64 particles are 4 tiles of 16 (tile t = particles 16t .. 16t+15).
+// D layout: lane l holds points 4(l>>4) .. +3 of the block for particle 16t + (l&15).
+struct KdeOps {
+  float b[4];      // B operand of tile t (feature l>>4 of particle 16t + (l&15))
+  float negsq[4];  // -|x'|^2 of particle 16t + (l&15)
+};
+
+// features: nf (slot, scale) pairs; slot = LDS value column.
+__device__ __forceinline__ void kde_operands(const Lane& L, const int (&slots)[4], const float (&scl)[4],
+                                             int nf, KdeOps& o) {
+  const int g = L.lane >> 4, n = L.lane & 15;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    float sq = 0.f, mine = 0.f;
+    for (int f = 0; f < nf; ++f) {
+      const float v = scl[f] * L.vals[slots[f] * WAVE + 16 * t + n];
+      sq = fmaf(v, v, sq);
+      if (f == g) mine = 2.f * v;
+    }
+    o.b[t] = g < nf ? mine : (g == nf ? -1.f : 0.f);
+    o.negsq[t] = -sq;
+  }
+}
+
+// the lane's own particle: x'_k and -|x'|^2 exactly as kde_operands computes them
+__device__ __forceinline__ float kde_own(const Lane& L, const int (&slots)[4], const float (&scl)[4], int nf,
+                                         float (&xv)[4]) {
+  float sq = 0.f;
+  for (int f = 0; f < nf; ++f) {
+    const float v = scl[f] * vread(L, slots[f]);
+    xv[f] = v;
+    sq = fmaf(v, v, sq);
+  }
+  return -sq;
+}
+
+// VALU replica of one MFMA output element (point j of pack kq).
+__device__ __forceinline__ float kde_arg_replica(const float* __restrict__ kq, int j, const float (&xv)[4],
+                                                 float negsq, int nf) {
+  const float* base = kq + (j >> 4) * 64 + (j & 15);
+  float d = negsq;
+  for (int f = 0; f < nf; ++f) d = fmaf(base[16 * f], 2.f * xv[f], d);
+  return fmaf(base[16 * nf], -1.f, d);
+}
+
+// Sum of the lane's 4 tile partials across the 4 lane groups: lane l receives the total of
+// particle l (tile l>>4, column l&15).  Three cross-lane moves.
+__device__ __forceinline__ float kde_reduce_tiles(const float (&s)[4], int lane) {
+  const int h = lane >> 5, b = (lane >> 4) & 1;
+  float k0 = h ? s[2] : s[0], k1 = h ? s[3] : s[1];
+  const float o0 = h ? s[0] : s[2], o1 = h ? s[1] : s[3];
+  k0 += __shfl_xor(o0, 32);
+  k1 += __shfl_xor(o1, 32);
+  const float k = b ? k1 : k0, o = b ? k0 : k1;
+  return k + __shfl_xor(o, 16);
+}
+
+// per-lane partial sums of exp2(arg) over 16-point blocks [b0, b1) of pack kq
+__device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int b0, int b1, const KdeOps& o,
+                                              int lane, float (&s)[4]) {
+  f32x4 cin[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) cin[t] = f32x4{o.negsq[t], o.negsq[t], o.negsq[t], o.negsq[t]};
+  // four blocks per trip: their loads are in flight together (indices clamped, extra blocks
+  // of the last trip are loaded but not summed)
+  for (int b = b0; b < b1; b += 4) {
+    float a[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] = kq[min(b + u, b1 - 1) * 64 + lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (b + u < b1) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], o.b[t], cin[t], 0, 0, 0);
+          s[t] += (__builtin_amdgcn_exp2f(d[0]) + __builtin_amdgcn_exp2f(d[1])) +
+                  (__builtin_amdgcn_exp2f(d[2]) + __builtin_amdgcn_exp2f(d[3]));
+        }
+      }
+    }
+  }
+}
+
+// Latent non-root KDE node, parent dims 1..3: index ~ softmax_j log K_p (kde.py:172-178).
+// Pass 1 (MFMA): per-chunk weight sums -> scr[chunk][lane]; pass 2 (VALU replica): locate the
+// chunk holding u * total, scan it.  All-underflow particles (every weight 0) redo the sums on
+// VALU relative to their largest weight.
+__device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
+                                              float ucat, float c_p) {
+  const float* __restrict__ kq = L.P + st.reserved[1];
+  const int M = st.k, nf = st.aux0, lane = L.lane;
+  const int nblk = (M + 15) >> 4, cb = (nblk + KDE_CHUNKS - 1) / KDE_CHUNKS;
+  int slots[4] = {0, 0, 0, 0};
+  float scl[4] = {c_p, c_p, c_p, c_p};
+  for (int f = 0; f < nf; ++f) slots[f] = L.ic[st.in_off + f];
+  KdeOps o;
+  kde_operands(L, slots, scl, nf, o);
+  double tot = 0.0;
+  for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+    const int b0 = min(nblk, ch * cb), b1 = min(nblk, b0 + cb);
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    kde_mfma_sums(kq, b0, b1, o, lane, s);
+    const float cs = kde_reduce_tiles(s, lane);
+    L.scr[ch * WAVE + lane] = cs;
+    tot += (double)cs;
+  }
+  float xv[4] = {0.f, 0.f, 0.f, 0.f};
+  const float negsq = kde_own(L, slots, scl, nf, xv);
+  float shift = 0.f;
+  if (!(tot > 0.0)) {                                 // every weight underflowed (or NaN parent)
+    float amax = -INFINITY;
+    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_replica(kq, j, xv, negsq, nf));
+    shift = amax;
+    tot = 0.0;
+    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+      const int j0 = min(M, ch * cb * 16), j1 = min(M, j0 + cb * 16);
+      float cs = 0.f;
+      for (int j = j0; j < j1; ++j) cs += __builtin_amdgcn_exp2f(kde_arg_replica(kq, j, xv, negsq, nf) - shift);
+      L.scr[ch * WAVE + lane] = cs;
+      tot += (double)cs;
+    }
+  }
+  const double thr = (double)ucat * tot;
+  double cum = 0.0;
+  int ch = KDE_CHUNKS - 1;
+  for (int c2 = 0; c2 < KDE_CHUNKS; ++c2) {
+    const double nx = cum + (double)L.scr[c2 * WAVE + lane];
+    if (nx > thr) { ch = c2; break; }
+    cum = nx;
+  }
+  const int j0 = min(M, ch * cb * 16), j1 = min(M, j0 + cb * 16);
+  const float rem = (float)(thr - cum);
+  int idx = max(j1 - 1, 0);
+  // scan the chunk over per-point records (16 B each, same values as the MFMA pack), 4 points
+  // per trip with the next 4 in flight; the host pads the records by >= 4 weight-0 rows
+  const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]);
+  const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
+  float cs = 0.f;
+  float4 r[4], rn[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) r[u] = rec[j0 + u];
+  for (int j = j0; j < j1; j += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rn[u] = rec[min(j + 4, j1 - 1) + u];
+    int hit = -1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float d = negsq;                                        // kde_arg_replica, nf in 1..3
+      d = fmaf(r[u].x, xb0, d);
+      d = nf > 1 ? fmaf(r[u].y, xb1, d) : d;
+      d = nf > 2 ? fmaf(r[u].z, xb2, d) : d;
+      const float y2 = nf == 1 ? r[u].y : (nf == 2 ? r[u].z : r[u].w);
+      d = fmaf(y2, -1.f, d);
+      cs += __builtin_amdgcn_exp2f(d - shift);
+      if (hit < 0 && cs > rem) hit = u;
+    }
+    if (hit >= 0) { idx = min(j + hit, j1 - 1); break; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[u] = rn[u];
+  }
+  wave_sync();
+  return idx;
+}
+
+// log p(x | parents) of a KDE node on MFMA (kde.py:114-146):
+//   root:     LSE_j log K_y - log M
+//   non-root: LSE_j (log K_p + log K_y) - LSE_j log K_p
+// pack kq (parent features) and kqy (parent ++ target features, scales c_p / c_y).  Returns
+// false (nothing added) when a sum underflows; the caller then takes the shifted VALU path.
+__device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L, bool root, float c_p,
+                                              float c_y, float cy, float log_n, float& lp) {
+  const int M = st.k, dp = st.aux0, D = st.out_dim, lane = L.lane;
+  const int nblk = (M + 15) >> 4;
+  int slots[4] = {0, 0, 0, 0};
+  float scl[4] = {c_p, c_p, c_p, c_p};
+  for (int f = 0; f < dp; ++f) slots[f] = L.ic[st.in_off + f];
+  for (int d = 0; d < D; ++d) { slots[dp + d] = st.out_col + d; scl[dp + d] = c_y; }
+  KdeOps oy;
+  kde_operands(L, slots, scl, dp + D, oy);
+  float sy4[4] = {0.f, 0.f, 0.f, 0.f}, sp4[4] = {0.f, 0.f, 0.f, 0.f};
+  kde_mfma_sums(L.P + st.reserved[2], 0, nblk, oy, lane, sy4);
+  const float sy = kde_reduce_tiles(sy4, lane);
+  float sp = 1.f;
+  if (!root) {
+    KdeOps op;
+    kde_operands(L, slots, scl, dp, op);
+    kde_mfma_sums(L.P + st.reserved[1], 0, nblk, op, lane, sp4);
+    sp = kde_reduce_tiles(sp4, lane);
+  }
+  wave_sync();
+  if (!(sy > 0.f) || !(sp > 0.f)) return false;
+  lp += root ? (__logf(sy) + cy - log_n) : ((__logf(sy) - __logf(sp)) + cy);
+  return true;
+}
+
 template <int DP, int DY>
 __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
 #pragma clang fp contract(off)
@@ -734,6 +939,7 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
   const int M = st.k, dp = DP >= 0 ? DP : st.aux0, stride = st.aux1, D = DY > 0 ? DY : st.out_dim;
   const float* t = P + st.off_tail;
   const float inv_sp = t[0], inv_sy = t[1], noise_scale = t[2], cy = t[3], log_n = t[4];
+  const float c_p = t[5], c_y = t[6];
   const bool root = (st.flags & VBN_F_ROOT) != 0;
   const int lane = L.lane;
   float pv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -745,6 +951,8 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
     int idx;
     if (root) {
       idx = min((int)(ucat * (float)M), M - 1);             // randint(0, M)
+    } else if (st.reserved[1] >= 0) {
+      idx = kde_index_mfma(A, st, L, ucat, c_p);
     } else {
       // pass 1: per-chunk weight sums -> scr[chunk][lane]
       const int csz = (M + KDE_CHUNKS - 1) / KDE_CHUNKS;
@@ -801,6 +1009,10 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
     for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
   }
 
+  if ((st.flags & VBN_F_LOGP) && st.reserved[2] >= 0 && (root || st.reserved[1] >= 0)) {
+    wave_sync();
+    if (kde_logp_mfma(st, L, root, c_p, c_y, cy, log_n, lp)) return;
+  }
   if (st.flags & VBN_F_LOGP) {
     const float x0 = NODE_X(0);
     float sy = 0.f, sp = 0.f, qymin = INFINITY, qpmin = INFINITY, qsmin = INFINITY;

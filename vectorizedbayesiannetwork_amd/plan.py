@@ -36,7 +36,7 @@ MODE_MCM, MODE_WEIGHTED, MODE_SAMPLE = 0, 1, 2
 STEP_INTS = 32
 (S_KIND, S_ROLE, S_FLAGS, S_ACT, S_NIN, S_INOFF, S_OUTCOL, S_OUTDIM, S_FIXEDCOL, S_K, S_NOUT,
  S_NODEID, S_NOISE, S_AUX0, S_AUX1, S_AUX2, S_OFF_STD, S_OFF_W1, S_OFF_W2, S_OFF_B2, S_OFF_W3,
- S_OFF_B3, S_OFF_TAIL, S_OFF_PTS, S_OFF_W2H) = range(25)
+ S_OFF_B3, S_OFF_TAIL, S_OFF_PTS, S_OFF_W2H, S_OFF_KQ, S_OFF_KQY, S_OFF_KR) = range(28)
 KDE_CHUNKS = 16
 MLP_HIDDEN = (32, 32)
 KDE_MAX_DIMS = 4
@@ -67,6 +67,28 @@ class _Blob:
 
     def finish(self) -> np.ndarray:
         return np.concatenate(self.parts) if self.parts else np.zeros(4, np.float32)
+
+
+_KDE_C = math.sqrt(0.5 * math.log2(math.e))      # exp(-d^2 / 2) = exp2(-(c d)^2)
+
+
+def _kde_pack(feats: List[np.ndarray], records: bool = False) -> np.ndarray:
+    """MFMA A-operand image of KDE points: [ceil(M/16)][4][16] fp32, features y'_k then |y'|^2.
+
+    Padding points get |y'|^2 = 1e30, i.e. weight exp2(-1e30) = 0.  ``records=True`` gives the
+    same values as per-point rows [16 ceil(M/16) + 4][4] (the kernel's inverse-CDF scan reads
+    up to 3 rows past a chunk end).
+    """
+    y = np.concatenate([f.reshape(f.shape[0], -1) for f in feats], axis=1).astype(np.float32)
+    m, nf = y.shape
+    nblk = (m + 15) // 16
+    a = np.zeros((nblk * 16 + 4, 4), np.float32)
+    a[:m, :nf] = y
+    a[:m, nf] = (y.astype(np.float64) ** 2).sum(axis=1).astype(np.float32)
+    a[m:, nf] = 1e30
+    if records:
+        return a
+    return a[:nblk * 16].reshape(nblk, 16, 4).transpose(0, 2, 1)
 
 
 def _np(t: torch.Tensor) -> np.ndarray:
@@ -198,8 +220,16 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
         s_y = max(bw, 1e-3) + min_scale
         noise_scale = max(bw, 1e-3) + min_scale            # kde.py:166,180
         cy = -0.5 * D * (math.log(2 * math.pi) + 2 * math.log(s_y))
+        c_p = np.float32(_KDE_C / s_p)
+        c_y = np.float32(_KDE_C / s_y)
         offs["tail"] = blob.add(np.array([1.0 / np.float32(s_p), 1.0 / np.float32(s_y),
-                                          noise_scale, cy, math.log(float(m)), 0, 0, 0], np.float32))
+                                          noise_scale, cy, math.log(float(m)), c_p, c_y, 0], np.float32))
+        # MFMA packs (csrc/vbn_walk.hip, kde_mfma_sums): [block][k][16] point features
+        if 1 <= dp <= 3:
+            offs["kq"] = blob.add(_kde_pack([_np(pts_p) * c_p]))
+            offs["kr"] = blob.add(_kde_pack([_np(pts_p) * c_p], records=True))
+        if dp + D <= 3:
+            offs["kqy"] = blob.add(_kde_pack(([_np(pts_p) * c_p] if dp else []) + [_np(pts_y) * c_y]))
         stride = dp + D
         stride += (-stride) % 2 if stride > 1 else 0
         recs = np.zeros((m, stride), np.float32)
@@ -393,6 +423,9 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
                          ("w3", S_OFF_W3), ("b3", S_OFF_B3), ("tail", S_OFF_TAIL), ("pts", S_OFF_PTS),
                          ("w2h", S_OFF_W2H)):
             row[idx] = npk.offs.get(key, 0)
+        row[S_OFF_KQ] = npk.offs.get("kq", -1)
+        row[S_OFF_KQY] = npk.offs.get("kqy", -1)
+        row[S_OFF_KR] = npk.offs.get("kr", -1)
     out_cols: List[int] = []
     for n in out_nodes:
         out_cols.extend(range(slot_of[n], slot_of[n] + model.out_dim(n)))
