@@ -111,7 +111,8 @@ def cpu_baseline(cfg, model, query, n_queries: int, reps: int = 3):
             else:
                 O.importance_sampling(model, query["target"], ev, {}, S, O.TorchDraws())
 
-    one()
+    if reps > 1:
+        one()
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -119,7 +120,8 @@ def cpu_baseline(cfg, model, query, n_queries: int, reps: int = 3):
         ts.append(time.perf_counter() - t0)
     med = statistics.median(ts)
     return {"value": n_queries / med, "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"{n_queries} queries x {S} samples, median of {reps} after 1 warm-up, "
+            "sample": f"{n_queries} queries x {S} samples, median of {reps}"
+                      f"{' after 1 warm-up' if reps > 1 else ''}, "
                       f"torch CPU {threads} threads, no_grad"}
 
 
@@ -145,6 +147,7 @@ def main():
     ap.add_argument("--cpu-queries", type=int, default=0)
     ap.add_argument("--prune-barren", action="store_true")
     ap.add_argument("--exact-f32", action="store_true", help="hidden layer on the exact f32 MFMA chain")
+    ap.add_argument("--kde-valu", action="store_true", help="KDE distances on packed VALU (default: 16x16x4 f32 MFMA tile)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -162,7 +165,7 @@ def main():
     cfg, g, model, vbn, query = build_workload(args.config, device, rank)
     B, S = cfg["B"], cfg["S"]
     vbn.set_inference_method(cfg["engine"], n_samples=S, q_base=rank * B,
-                             prune_barren=args.prune_barren, exact_f32=args.exact_f32)
+                             prune_barren=args.prune_barren, exact_f32=args.exact_f32, kde_valu=args.kde_valu)
     if cfg["engine"] == "importance_sampling":
         vbn._inference._lw.q_base = rank * B
 
@@ -213,8 +216,7 @@ def main():
     traffic = load_traffic(args.config)
     kern_s = kern_ms * 1e-3
     if exps > 0.1 * flops / 64:
-        # KDE: one exp per (particle, point) kernel weight; distances on MFMA (16x16x4 f32), the
-        # bound is the v_exp_f32 issue rate
+        # KDE: one exp per (particle, point) kernel weight; the bound is the v_exp_f32 issue rate
         ach = exps / kern_s / 1e12
         roof = {"bound": "exp", "achieved": round(ach, 4), "peak": round(EXP_PEAK_T, 2), "unit": "Texp/s",
                 "frac": round(ach / EXP_PEAK_T, 4), "traffic": traffic, "kernel": "vbn_walk_kernel",
@@ -250,13 +252,15 @@ def main():
         "config": {"workload": f"{args.config}: {cfg['name']}", "queries_per_gpu": B, "global_batch": B * world,
                    "n_samples": S, "n_nodes": cfg["n_nodes"], "engine": cfg["engine"],
                    "parallelism": f"query-sharded dp{world}", "prune_barren": args.prune_barren,
-                   "exact_f32": args.exact_f32},
+                   "exact_f32": args.exact_f32, "kde_distances": "valu" if args.kde_valu else "mfma"},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        kde = "kde" in cfg["kinds"]
         nq = args.cpu_queries or (1024 if cfg["engine"] == "monte_carlo_marginalization" and cfg["n_nodes"] <= 64
-                                  and "kde" not in cfg["kinds"] else 8)
-        out["cpu_baseline"] = cpu_baseline(cfg, model, query, nq)
+                                  and not kde else (1 if kde else 8))
+        print(f"cpu baseline: {nq} queries on the host ...", file=sys.stderr, flush=True)
+        out["cpu_baseline"] = cpu_baseline(cfg, model, query, nq, reps=1 if kde else 3)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -61,6 +61,7 @@ enum vbn_role { VBN_ROLE_SKIP = 0, VBN_ROLE_LATENT = 1, VBN_ROLE_FIXED = 2 };
 #define VBN_F_STANDARDIZE 8 /* MLP input (x-mean)/std (gaussian_nn)                          */
 #define VBN_F_CLIP 16       /* softmax_nn within_bin_clip                                      */
 #define VBN_F_F32L2 32      /* NN CPD: exact f32 MFMA chain for layer 2 instead of split-f16   */
+#define VBN_F_KDE_VALU 64   /* kde: pairwise distances on packed VALU (else the 16x16x4 f32 MFMA tile) */
 
 /* activations of the NN CPDs (reference gaussian_nn.py:19-24) */
 enum vbn_act { VBN_ACT_RELU = 0, VBN_ACT_TANH = 1, VBN_ACT_GELU = 2, VBN_ACT_ELU = 3 };

@@ -51,13 +51,18 @@ def _close(name, got, ref, atol, rtol):
 def _cases():
     out = []
     for name in golden_names():
-        for i, case in enumerate(load_golden(name)["cases"]):
-            out.append(pytest.param(name, i, id=f"{name}-{i}-{case['engine']}"))
+        fx = load_golden(name)
+        has_kde = any(str(v["cpd_key"]) == "kde" for v in fx["model"]["nodes"].values())
+        for i, case in enumerate(fx["cases"]):
+            out.append(pytest.param(name, i, False, id=f"{name}-{i}-{case['engine']}"))
+            if has_kde and case["engine"] != "cpd":
+                # the alternative KDE distance path (packed VALU)
+                out.append(pytest.param(name, i, True, id=f"{name}-{i}-{case['engine']}-kde_valu"))
     return out
 
 
-@pytest.mark.parametrize("name,idx", _cases())
-def test_golden_case_on_gpu(name, idx):
+@pytest.mark.parametrize("name,idx,kde_valu", _cases())
+def test_golden_case_on_gpu(name, idx, kde_valu):
     from vectorizedbayesiannetwork_amd import cpd as C
     from vectorizedbayesiannetwork_amd.engines import (AncestralSampler, ImportanceSampling,
                                                        LikelihoodWeighting, MonteCarloMarginalization)
@@ -85,19 +90,19 @@ def test_golden_case_on_gpu(name, idx):
     p = case["params"]
     draws = O.ReplayDraws(case["draws"])
     if eng == "monte_carlo_marginalization":
-        pdf, xs = MonteCarloMarginalization(n_samples=n).infer_posterior(vbn, qq, _noise=nd0)
+        pdf, xs = MonteCarloMarginalization(n_samples=n, kde_valu=kde_valu).infer_posterior(vbn, qq, _noise=nd0)
         rpdf, rxs = O.monte_carlo_marginalization(model, q["target"], q["evidence"], q["do"], n, draws)
         _close("samples", xs, rxs, S_ATOL, S_RTOL)
         _close("pdf", pdf, rpdf, P_ATOL, P_RTOL)
     elif eng == "likelihood_weighting":
-        e = LikelihoodWeighting(n_samples=n, normalize=p.get("normalize", True))
+        e = LikelihoodWeighting(n_samples=n, normalize=p.get("normalize", True), kde_valu=kde_valu)
         w, xs = e.infer_posterior(vbn, qq, _noise=nd0)
         rw, rxs = O.likelihood_weighting(model, q["target"], q["evidence"], q["do"], n, draws,
                                          normalize=p.get("normalize", True))
         _close("samples", xs, rxs, S_ATOL, S_RTOL)
         _close("weights", w, rw, P_ATOL, P_RTOL)
     elif eng == "importance_sampling":
-        e = ImportanceSampling(n_samples=n)
+        e = ImportanceSampling(n_samples=n, kde_valu=kde_valu)
         e.ess_threshold = p.get("ess_threshold", 0.1)
         w, xs = e.infer_posterior(vbn, qq, _noise=nd0, _noise_fallback=noise_dict(case, model, 1))
         rw, rxs, ress, rfb = O.importance_sampling(model, q["target"], q["evidence"], q["do"], n, draws,
@@ -107,7 +112,7 @@ def test_golden_case_on_gpu(name, idx):
         _close("samples", xs, rxs, S_ATOL, S_RTOL)
         _close("weights", w, rw, P_ATOL, P_RTOL)
     elif eng == "ancestral":
-        xs = AncestralSampler(n_samples=n).sample(vbn, qq, n, _noise=nd0)
+        xs = AncestralSampler(n_samples=n, kde_valu=kde_valu).sample(vbn, qq, n, _noise=nd0)
         rxs = O.ancestral(model, q["target"], q["evidence"], q["do"], n, draws)
         _close("samples", xs, rxs, S_ATOL, S_RTOL)
     else:

@@ -730,19 +730,22 @@ __device__ __forceinline__ float kde_qy(const float* __restrict__ pty, float x0,
 // ---- pairwise kernel weights on MFMA ------------------------------------------------------
 // The kernel weight of particle n and stored point m is exp(-|x_n - y_m|^2 / (2 s^2)) =
 // exp2(-|x'_n - y'_m|^2) with x' = c x, y' = c y, c = sqrt(log2(e) / 2) / s, and
-//   -|x' - y'|^2 = -|x'|^2 + sum_k (2 x'_k) y'_k - |y'|^2,
-// a contraction over K = nf + 1 <= 4 features: one v_mfma_f32_16x16x4_f32 per 16 points x 16
-// particles with A[m][k] = (y'_0 .. y'_{nf-1}, |y'|^2, 0..) (host-packed as [block][k][16],
-// padding points |y'|^2 = 1e30 -> weight 0), B[k][n] = (2x'_0 .. 2x'_{nf-1}, -1, 0..) and the
-// accumulator input C = -|x'_n|^2.  The MFMA is a k-ordered fmaf chain from C, so
-// kde_arg_replica() reproduces any element bit-for-bit on VALU (the inverse-CDF scan).
-// The wave's 64 particles are 4 tiles of 16 (tile t = particles 16t .. 16t+15).
-// D layout: lane l holds points 4(l>>4) .. +3 of the block for particle 16t + (l&15).
+//   -|x' - y'|^2 = sum_k (2 x'_k) y'_k - |y'|^2 - |x'|^2,
+// a contraction over K <= 4 features: one v_mfma_f32_16x16x4_f32 per 16 points x 16 particles
+// (A = point features, host-packed as [block][k][16]; B = particle features; see KdeOps for
+// the two operand forms).  Padding points have |y'|^2 = 1e30 -> weight 0.  The MFMA is a
+// k-ordered fmaf chain from C, so kde_arg_rec() reproduces any element bit-for-bit on VALU
+// (the inverse-CDF scan).  The wave's 64 particles are 4 tiles of 16 (tile t = particles
+// 16t .. 16t+15); D layout: lane l holds points 4(l>>4) .. +3 of the block for particle
+// 16t + (l&15).  Bound: v_exp_f32 issue (one exp per pair); MFMA pipe 32 cycles per 256 pairs.
 struct KdeOps {
   float b[4];      // B operand of tile t (feature l>>4 of particle 16t + (l&15))
   float negsq[4];  // -|x'|^2 of particle 16t + (l&15)
 };
 
+// Two operand forms, chosen by the feature count nf (host packs match, plan.py _kde_pack):
+//   nf <= 2 ("ZC"): K = nf + 2, A = (y'.., |y'|^2, 1), B = (2x'.., -1, -|x'|^2), C = 0
+//   nf == 3       : K = 4,      A = (y'.., |y'|^2),    B = (2x'.., -1),          C = -|x'|^2
 // features: nf (slot, scale) pairs; slot = LDS value column.
 __device__ __forceinline__ void kde_operands(const Lane& L, const int (&slots)[4], const float (&scl)[4],
                                              int nf, KdeOps& o) {
@@ -755,7 +758,7 @@ __device__ __forceinline__ void kde_operands(const Lane& L, const int (&slots)[4
       sq = fmaf(v, v, sq);
       if (f == g) mine = 2.f * v;
     }
-    o.b[t] = g < nf ? mine : (g == nf ? -1.f : 0.f);
+    o.b[t] = g < nf ? mine : (g == nf ? -1.f : ((g == nf + 1 && nf <= 2) ? -sq : 0.f));
     o.negsq[t] = -sq;
   }
 }
@@ -772,13 +775,24 @@ __device__ __forceinline__ float kde_own(const Lane& L, const int (&slots)[4], c
   return -sq;
 }
 
-// VALU replica of one MFMA output element (point j of pack kq).
-__device__ __forceinline__ float kde_arg_replica(const float* __restrict__ kq, int j, const float (&xv)[4],
-                                                 float negsq, int nf) {
-  const float* base = kq + (j >> 4) * 64 + (j & 15);
-  float d = negsq;
-  for (int f = 0; f < nf; ++f) d = fmaf(base[16 * f], 2.f * xv[f], d);
-  return fmaf(base[16 * nf], -1.f, d);
+// VALU replica of one MFMA output element (k-ordered fmaf chain from C), point record r =
+// (y'_0 .. y'_{nf-1}, |y'|^2, ..) of the per-point record pack.
+__device__ __forceinline__ float kde_arg_rec(const float4 r, float xb0, float xb1, float xb2, float negsq,
+                                             int nf) {
+  const bool zc = nf <= 2;
+  float d = zc ? 0.f : negsq;
+  d = fmaf(r.x, xb0, d);
+  d = nf > 1 ? fmaf(r.y, xb1, d) : d;
+  d = nf > 2 ? fmaf(r.z, xb2, d) : d;
+  const float y2 = nf == 1 ? r.y : (nf == 2 ? r.z : r.w);
+  d = fmaf(y2, -1.f, d);
+  return zc ? fmaf(1.f, negsq, d) : d;
+}
+
+// Blocks per chunk: a multiple of 4 (the host pads the pack to KDE_CHUNKS * kde_cb(M) blocks).
+__device__ __forceinline__ int kde_cb(int M) {
+  const int nblk = (M + 15) >> 4;
+  return (((nblk + KDE_CHUNKS - 1) / KDE_CHUNKS) + 3) & ~3;
 }
 
 // Sum of the lane's 4 tile partials across the 4 lane groups: lane l receives the total of
@@ -793,30 +807,43 @@ __device__ __forceinline__ float kde_reduce_tiles(const float (&s)[4], int lane)
   return k + __shfl_xor(o, 16);
 }
 
-// per-lane partial sums of exp2(arg) over 16-point blocks [b0, b1) of pack kq
+// per-lane partial sums of exp2(arg) over 16-point blocks [b0, b1) of pack kq, b1 - b0 a
+// multiple of 4 (padding blocks have weight 0); sums in packed pairs (v_pk_add_f32)
+template <bool ZC>
 __device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int b0, int b1, const KdeOps& o,
                                               int lane, float (&s)[4]) {
   f32x4 cin[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) cin[t] = f32x4{o.negsq[t], o.negsq[t], o.negsq[t], o.negsq[t]};
-  // four blocks per trip: their loads are in flight together (indices clamped, extra blocks
-  // of the last trip are loaded but not summed)
+  for (int t = 0; t < 4; ++t)
+    cin[t] = ZC ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4{o.negsq[t], o.negsq[t], o.negsq[t], o.negsq[t]};
+  f32x2 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x2{0.f, 0.f};
   for (int b = b0; b < b1; b += 4) {
     float a[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] = kq[min(b + u, b1 - 1) * 64 + lane];
+    for (int u = 0; u < 4; ++u) a[u] = kq[(b + u) * 64 + lane];   // four loads in flight
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (b + u < b1) {
+      f32x4 d[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], o.b[t], cin[t], 0, 0, 0);
-          s[t] += (__builtin_amdgcn_exp2f(d[0]) + __builtin_amdgcn_exp2f(d[1])) +
-                  (__builtin_amdgcn_exp2f(d[2]) + __builtin_amdgcn_exp2f(d[3]));
-        }
+      for (int t = 0; t < 4; ++t) d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], o.b[t], cin[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const f32x2 e01 = f32x2{__builtin_amdgcn_exp2f(d[t][0]), __builtin_amdgcn_exp2f(d[t][1])};
+        const f32x2 e23 = f32x2{__builtin_amdgcn_exp2f(d[t][2]), __builtin_amdgcn_exp2f(d[t][3])};
+        acc[t] += e01 + e23;
       }
     }
   }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) s[t] += acc[t].x + acc[t].y;
+}
+
+__device__ __forceinline__ void kde_sums(const float* __restrict__ kq, int b0, int b1, const KdeOps& o, int nf,
+                                         int lane, float (&s)[4]) {
+  if (nf <= 2) kde_mfma_sums<true>(kq, b0, b1, o, lane, s);
+  else kde_mfma_sums<false>(kq, b0, b1, o, lane, s);
 }
 
 // Latent non-root KDE node, parent dims 1..3: index ~ softmax_j log K_p (kde.py:172-178).
@@ -827,7 +854,7 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
                                               float ucat, float c_p) {
   const float* __restrict__ kq = L.P + st.reserved[1];
   const int M = st.k, nf = st.aux0, lane = L.lane;
-  const int nblk = (M + 15) >> 4, cb = (nblk + KDE_CHUNKS - 1) / KDE_CHUNKS;
+  const int cb = kde_cb(M);
   int slots[4] = {0, 0, 0, 0};
   float scl[4] = {c_p, c_p, c_p, c_p};
   for (int f = 0; f < nf; ++f) slots[f] = L.ic[st.in_off + f];
@@ -835,25 +862,28 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   kde_operands(L, slots, scl, nf, o);
   double tot = 0.0;
   for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-    const int b0 = min(nblk, ch * cb), b1 = min(nblk, b0 + cb);
     float s[4] = {0.f, 0.f, 0.f, 0.f};
-    kde_mfma_sums(kq, b0, b1, o, lane, s);
+    kde_sums(kq, ch * cb, ch * cb + cb, o, nf, lane, s);
     const float cs = kde_reduce_tiles(s, lane);
     L.scr[ch * WAVE + lane] = cs;
     tot += (double)cs;
   }
   float xv[4] = {0.f, 0.f, 0.f, 0.f};
   const float negsq = kde_own(L, slots, scl, nf, xv);
+  const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
+  // per-point records, 4 weight-0 rows before the first point, >= 4 after the last
+  const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
   float shift = 0.f;
   if (!(tot > 0.0)) {                                 // every weight underflowed (or NaN parent)
     float amax = -INFINITY;
-    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_replica(kq, j, xv, negsq, nf));
+    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nf));
     shift = amax;
     tot = 0.0;
     for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
       const int j0 = min(M, ch * cb * 16), j1 = min(M, j0 + cb * 16);
       float cs = 0.f;
-      for (int j = j0; j < j1; ++j) cs += __builtin_amdgcn_exp2f(kde_arg_replica(kq, j, xv, negsq, nf) - shift);
+      for (int j = j0; j < j1; ++j)
+        cs += __builtin_amdgcn_exp2f(kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nf) - shift);
       L.scr[ch * WAVE + lane] = cs;
       tot += (double)cs;
     }
@@ -868,31 +898,35 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   }
   const int j0 = min(M, ch * cb * 16), j1 = min(M, j0 + cb * 16);
   const float rem = (float)(thr - cum);
-  int idx = max(j1 - 1, 0);
-  // scan the chunk over per-point records (16 B each, same values as the MFMA pack), 4 points
-  // per trip with the next 4 in flight; the host pads the records by >= 4 weight-0 rows
-  const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]);
-  const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
+  const float csum = L.scr[ch * WAVE + lane];
+  // Scan the chunk over the records, 4 points per trip with the next 4 in flight.  A lane
+  // whose threshold lies in the upper half of its chunk scans backwards from the end for the
+  // right-hand mass csum - rem: the point found is the same (the largest j with
+  // cum(j-1) <= rem), and no lane scans more than about half a chunk.
+  const bool back = rem > 0.5f * csum;
+  const float goal = back ? csum - rem : rem;
+  const int step = back ? -4 : 4;
+  const int nb16 = ((M + 15) >> 4) * 16;           // records valid on [-4, nb16 + 4)
+  int j = back ? j1 - 4 : j0;                      // first record of the current trip
+  int idx = back ? j0 : max(j1 - 1, 0);
   float cs = 0.f;
   float4 r[4], rn[4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) r[u] = rec[j0 + u];
-  for (int j = j0; j < j1; j += 4) {
+  for (int u = 0; u < 4; ++u) r[u] = rec[j + u];
+  for (int it = 0; it < (j1 - j0 + 3) / 4; ++it, j += step) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) rn[u] = rec[min(j + 4, j1 - 1) + u];
+    for (int u = 0; u < 4; ++u) rn[u] = rec[min(max(j + step, -4), nb16) + u];
     int hit = -1;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float d = negsq;                                        // kde_arg_replica, nf in 1..3
-      d = fmaf(r[u].x, xb0, d);
-      d = nf > 1 ? fmaf(r[u].y, xb1, d) : d;
-      d = nf > 2 ? fmaf(r[u].z, xb2, d) : d;
-      const float y2 = nf == 1 ? r[u].y : (nf == 2 ? r[u].z : r[u].w);
-      d = fmaf(y2, -1.f, d);
-      cs += __builtin_amdgcn_exp2f(d - shift);
-      if (hit < 0 && cs > rem) hit = u;
+    for (int v = 0; v < 4; ++v) {
+      const int u = back ? 3 - v : v;
+      const float d = kde_arg_rec(r[u], xb0, xb1, xb2, negsq, nf);
+      const int jj = j + u;
+      const bool inside = back ? jj >= j0 : jj < j1;
+      cs += inside ? __builtin_amdgcn_exp2f(d - shift) : 0.f;
+      if (hit < 0 && inside && (back ? cs >= goal : cs > goal)) hit = jj;
     }
-    if (hit >= 0) { idx = min(j + hit, j1 - 1); break; }
+    if (hit >= 0) { idx = hit; break; }
 #pragma unroll
     for (int u = 0; u < 4; ++u) r[u] = rn[u];
   }
@@ -908,27 +942,145 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
 __device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L, bool root, float c_p,
                                               float c_y, float cy, float log_n, float& lp) {
   const int M = st.k, dp = st.aux0, D = st.out_dim, lane = L.lane;
-  const int nblk = (M + 15) >> 4;
+  const int nb = (((M + 15) >> 4) + 3) & ~3;
   int slots[4] = {0, 0, 0, 0};
   float scl[4] = {c_p, c_p, c_p, c_p};
   for (int f = 0; f < dp; ++f) slots[f] = L.ic[st.in_off + f];
   for (int d = 0; d < D; ++d) { slots[dp + d] = st.out_col + d; scl[dp + d] = c_y; }
-  KdeOps oy;
-  kde_operands(L, slots, scl, dp + D, oy);
   float sy4[4] = {0.f, 0.f, 0.f, 0.f}, sp4[4] = {0.f, 0.f, 0.f, 0.f};
-  kde_mfma_sums(L.P + st.reserved[2], 0, nblk, oy, lane, sy4);
+  {
+    KdeOps oy;
+    kde_operands(L, slots, scl, dp + D, oy);
+    kde_sums(L.P + st.reserved[2], 0, nb, oy, dp + D, lane, sy4);
+  }
   const float sy = kde_reduce_tiles(sy4, lane);
   float sp = 1.f;
   if (!root) {
     KdeOps op;
     kde_operands(L, slots, scl, dp, op);
-    kde_mfma_sums(L.P + st.reserved[1], 0, nblk, op, lane, sp4);
+    kde_sums(L.P + st.reserved[1], 0, nb, op, dp, lane, sp4);
     sp = kde_reduce_tiles(sp4, lane);
   }
   wave_sync();
   if (!(sy > 0.f) || !(sp > 0.f)) return false;
   lp += root ? (__logf(sy) + cy - log_n) : ((__logf(sy) - __logf(sp)) + cy);
   return true;
+}
+
+// ---- pairwise kernel weights on VALU (alternative path, VBN_F_KDE_VALU) ---------------------
+// -|x' - y'|^2 with packed f32 VALU (v_pk_add / v_pk_mul / v_pk_fma on two points per lane),
+// points wave-uniform from scalar loads.  Measured on MI355X (cfg4, 64-node KDE, M = 10k,
+// 4096 x 1024 particles): 253 ms per walk vs 245 ms with the MFMA distance tile (and 266 ms
+// with the scalar loads software-pipelined), so the MFMA tile is the default.
+// Pack kv (plan.py _kde_pack_valu): [KDE_CHUNKS * csz / 8][NF][8] fp32, padding points
+// y' = 1e15 (weight 0).  Chunk ch = points [ch * csz, (ch + 1) * csz).
+__device__ __forceinline__ int kde_csz(int M) { return (((M + KDE_CHUNKS - 1) / KDE_CHUNKS) + 7) & ~7; }
+
+// -|x' - y'|^2 of one point record r = (y'_0, y'_1, y'_2, .); same operations, same order as
+// the packed pass (bit-identical per element)
+template <int NF>
+__device__ __forceinline__ float kde_arg_valu(const float (&xv)[4], const float4 r) {
+#pragma clang fp contract(off)
+  const float d0 = xv[0] - r.x;
+  float a = d0 * d0;
+  if (NF > 1) { const float d1 = xv[1] - r.y; a = fmaf(d1, d1, a); }
+  if (NF > 2) { const float d2 = xv[2] - r.z; a = fmaf(d2, d2, a); }
+  return -a;
+}
+
+template <int NF>
+__device__ __forceinline__ int kde_index_valu(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
+                                              float ucat, float c_p) {
+#pragma clang fp contract(off)
+  const float* __restrict__ kv = L.P + st.reserved[4];
+  const int M = st.k, lane = L.lane, csz = kde_csz(M);
+  float xv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int f = 0; f < NF; ++f) xv[f] = c_p * vread(L, L.ic[st.in_off + f]);
+  f32x2 xp[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) xp[f] = f32x2{xv[f], xv[f]};
+  double tot = 0.0;
+  for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+    const float* __restrict__ blk = kv + (int64_t)(ch * (csz >> 3)) * (NF * 8);
+    f32x2 acc = f32x2{0.f, 0.f};
+    for (int b = 0; b < (csz >> 3); ++b, blk += NF * 8) {
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        const f32x2 d0 = xp[0] - f32x2{blk[i], blk[i + 1]};
+        f32x2 a = d0 * d0;
+        if (NF > 1) {
+          const f32x2 d1 = xp[1] - f32x2{blk[8 + i], blk[8 + i + 1]};
+          a = __builtin_elementwise_fma(d1, d1, a);
+        }
+        if (NF > 2) {
+          const f32x2 d2 = xp[2] - f32x2{blk[16 + i], blk[16 + i + 1]};
+          a = __builtin_elementwise_fma(d2, d2, a);
+        }
+        acc += f32x2{__builtin_amdgcn_exp2f(-a.x), __builtin_amdgcn_exp2f(-a.y)};
+      }
+    }
+    const float cs = acc.x + acc.y;
+    L.scr[ch * WAVE + lane] = cs;
+    tot += (double)cs;
+  }
+  // per-point records, 4 weight-0 rows before the first point, >= 4 after the last
+  const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
+  float shift = 0.f;
+  if (!(tot > 0.0)) {                                 // every weight underflowed (or NaN parent)
+    float amax = -INFINITY;
+    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_valu<NF>(xv, rec[j]));
+    shift = amax;
+    tot = 0.0;
+    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+      const int j0 = min(M, ch * csz), j1 = min(M, j0 + csz);
+      float cs = 0.f;
+      for (int j = j0; j < j1; ++j) cs += __builtin_amdgcn_exp2f(kde_arg_valu<NF>(xv, rec[j]) - shift);
+      L.scr[ch * WAVE + lane] = cs;
+      tot += (double)cs;
+    }
+  }
+  const double thr = (double)ucat * tot;
+  double cum = 0.0;
+  int ch = KDE_CHUNKS - 1;
+  for (int c2 = 0; c2 < KDE_CHUNKS; ++c2) {
+    const double nx = cum + (double)L.scr[c2 * WAVE + lane];
+    if (nx > thr) { ch = c2; break; }
+    cum = nx;
+  }
+  const int j0 = min(M, ch * csz), j1 = min(M, j0 + csz);
+  const float rem = (float)(thr - cum);
+  const float csum = L.scr[ch * WAVE + lane];
+  // bidirectional chunk scan (see kde_index_mfma)
+  const bool back = rem > 0.5f * csum;
+  const float goal = back ? csum - rem : rem;
+  const int step = back ? -4 : 4;
+  const int nb16 = ((M + 15) >> 4) * 16;           // records valid on [-4, nb16 + 4)
+  int j = back ? j1 - 4 : j0;
+  int idx = back ? j0 : max(j1 - 1, 0);
+  float cs = 0.f;
+  float4 r[4], rn[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) r[u] = rec[j + u];
+  for (int it = 0; it < (j1 - j0 + 3) / 4; ++it, j += step) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rn[u] = rec[min(max(j + step, -4), nb16) + u];
+    int hit = -1;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int u = back ? 3 - v : v;
+      const float d = kde_arg_valu<NF>(xv, r[u]);
+      const int jj = j + u;
+      const bool inside = back ? jj >= j0 : jj < j1;
+      cs += inside ? __builtin_amdgcn_exp2f(d - shift) : 0.f;
+      if (hit < 0 && inside && (back ? cs >= goal : cs > goal)) hit = jj;
+    }
+    if (hit >= 0) { idx = hit; break; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) r[u] = rn[u];
+  }
+  wave_sync();
+  return idx;
 }
 
 template <int DP, int DY>
@@ -951,6 +1103,9 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
     int idx;
     if (root) {
       idx = min((int)(ucat * (float)M), M - 1);             // randint(0, M)
+    } else if (st.reserved[4] >= 0 && (st.flags & VBN_F_KDE_VALU)) {
+      idx = st.aux0 == 1 ? kde_index_valu<1>(A, st, L, ucat, c_p)
+          : (st.aux0 == 2 ? kde_index_valu<2>(A, st, L, ucat, c_p) : kde_index_valu<3>(A, st, L, ucat, c_p));
     } else if (st.reserved[1] >= 0) {
       idx = kde_index_mfma(A, st, L, ucat, c_p);
     } else {

@@ -205,16 +205,18 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
 
 class _EngineBase:
     def __init__(self, n_samples: int = 200, seed: Optional[int] = None, prune_barren: bool = False,
-                 q_base: int = 0, exact_f32: bool = False, **kwargs):
+                 q_base: int = 0, exact_f32: bool = False, kde_valu: bool = False, **kwargs):
         self.n_samples = int(n_samples)
         self.seed = seed
         self.prune_barren = bool(prune_barren)
         self.q_base = int(q_base)
         self.exact_f32 = bool(exact_f32)     # hidden layer on the exact f32 MFMA chain
+        self.kde_valu = bool(kde_valu)       # KDE distances on packed VALU (else the MFMA tile)
         self._calls = 0
 
     def _plan(self, pk, key, **kw):
-        return _plan(pk, key + (self.exact_f32,), exact_f32=self.exact_f32, **kw)
+        return _plan(pk, key + (self.exact_f32, self.kde_valu), exact_f32=self.exact_f32,
+                     kde_valu=self.kde_valu, **kw)
 
     def _seed(self, kwargs) -> int:
         if "seed" in kwargs and kwargs["seed"] is not None:
@@ -325,7 +327,7 @@ class ImportanceSampling(LikelihoodWeighting):
         self._last_fallback = False
         self._last_ess: Optional[torch.Tensor] = None
         self._lw = LikelihoodWeighting(n_samples=self.n_samples, q_base=self.q_base,
-                                       exact_f32=self.exact_f32)
+                                       exact_f32=self.exact_f32, kde_valu=self.kde_valu)
 
     def fallback_needed(self, ess: torch.Tensor, n: int) -> torch.Tensor:
         """Device-side flag (NaN ESS never triggers; importance_sampling.py:85-86)."""

@@ -29,14 +29,14 @@ from .model import BNModel, CPDRecord
 # ---- must match include/vbn_hip.h -------------------------------------------------------
 KIND_ID = {"gaussian_nn": 0, "linear_gaussian": 1, "mdn": 2, "kde": 3, "softmax_nn": 4}
 ROLE_SKIP, ROLE_LATENT, ROLE_FIXED = 0, 1, 2
-F_LOGP, F_ROOT, F_SHARED, F_STANDARDIZE, F_CLIP, F_F32L2 = 1, 2, 4, 8, 16, 32
+F_LOGP, F_ROOT, F_SHARED, F_STANDARDIZE, F_CLIP, F_F32L2, F_KDE_VALU = 1, 2, 4, 8, 16, 32, 64
 ACT_ID = {"relu": 0, "tanh": 1, "gelu": 2, "elu": 3}
 WITHIN_ID = {"uniform": 0, "triangular": 1, "gaussian": 2}
 MODE_MCM, MODE_WEIGHTED, MODE_SAMPLE = 0, 1, 2
 STEP_INTS = 32
 (S_KIND, S_ROLE, S_FLAGS, S_ACT, S_NIN, S_INOFF, S_OUTCOL, S_OUTDIM, S_FIXEDCOL, S_K, S_NOUT,
  S_NODEID, S_NOISE, S_AUX0, S_AUX1, S_AUX2, S_OFF_STD, S_OFF_W1, S_OFF_W2, S_OFF_B2, S_OFF_W3,
- S_OFF_B3, S_OFF_TAIL, S_OFF_PTS, S_OFF_W2H, S_OFF_KQ, S_OFF_KQY, S_OFF_KR) = range(28)
+ S_OFF_B3, S_OFF_TAIL, S_OFF_PTS, S_OFF_W2H, S_OFF_KQ, S_OFF_KQY, S_OFF_KR, S_OFF_KV) = range(29)
 KDE_CHUNKS = 16
 MLP_HIDDEN = (32, 32)
 KDE_MAX_DIMS = 4
@@ -72,23 +72,49 @@ class _Blob:
 _KDE_C = math.sqrt(0.5 * math.log2(math.e))      # exp(-d^2 / 2) = exp2(-(c d)^2)
 
 
-def _kde_pack(feats: List[np.ndarray], records: bool = False) -> np.ndarray:
-    """MFMA A-operand image of KDE points: [ceil(M/16)][4][16] fp32, features y'_k then |y'|^2.
+def _kde_cb(m: int) -> int:
+    """16-point blocks per inverse-CDF chunk (a multiple of 4; csrc kde_cb)."""
+    nblk = (m + 15) // 16
+    return ((nblk + KDE_CHUNKS - 1) // KDE_CHUNKS + 3) & ~3
 
-    Padding points get |y'|^2 = 1e30, i.e. weight exp2(-1e30) = 0.  ``records=True`` gives the
-    same values as per-point rows [16 ceil(M/16) + 4][4] (the kernel's inverse-CDF scan reads
-    up to 3 rows past a chunk end).
+
+def _kde_pack(feats: List[np.ndarray], records: bool = False) -> np.ndarray:
+    """KDE point features y' (scaled) for the kernel (csrc/vbn_walk.hip, kde_mfma_sums).
+
+    MFMA A-operand image: [KDE_CHUNKS * cb][4][16] fp32 (cb = _kde_cb(M) blocks per chunk),
+    columns (y'_0 .. y'_{nf-1}, |y'|^2, 1) for nf <= 2 and (y'_0, y'_1, y'_2, |y'|^2) for
+    nf == 3; padding points get |y'|^2 = 1e30, i.e. weight exp2(-1e30) = 0.
+    ``records=True``: per-point rows (y'.., |y'|^2) [4 + 16 ceil(M/16) + 4][4] with weight-0
+    rows before the first point and after the last (the inverse-CDF scan reads one trip of 4
+    past either end of a chunk).
     """
     y = np.concatenate([f.reshape(f.shape[0], -1) for f in feats], axis=1).astype(np.float32)
     m, nf = y.shape
+    if nf > 3:
+        raise ValueError("kde MFMA pack supports at most 3 features")
     nblk = (m + 15) // 16
-    a = np.zeros((nblk * 16 + 4, 4), np.float32)
-    a[:m, :nf] = y
-    a[:m, nf] = (y.astype(np.float64) ** 2).sum(axis=1).astype(np.float32)
-    a[m:, nf] = 1e30
+    rows = 4 + nblk * 16 + 4 if records else KDE_CHUNKS * _kde_cb(m) * 16
+    a = np.zeros((rows, 4), np.float32)
+    o = 4 if records else 0
+    a[:, nf] = 1e30
+    a[o:o + m, :nf] = y
+    a[o:o + m, nf] = (y.astype(np.float64) ** 2).sum(axis=1).astype(np.float32)
     if records:
         return a
-    return a[:nblk * 16].reshape(nblk, 16, 4).transpose(0, 2, 1)
+    if nf <= 2:
+        a[:, nf + 1] = 1.0
+    return a.reshape(rows // 16, 16, 4).transpose(0, 2, 1)
+
+
+def _kde_pack_valu(y: np.ndarray) -> np.ndarray:
+    """Point features y' for the VALU pass: [KDE_CHUNKS * csz / 8][nf][8] fp32 (csz = points
+    per chunk, a multiple of 8; csrc kde_csz); padding points y' = 1e15 (weight 0)."""
+    y = y.reshape(y.shape[0], -1).astype(np.float32)
+    m, nf = y.shape
+    csz = ((m + KDE_CHUNKS - 1) // KDE_CHUNKS + 7) & ~7
+    a = np.full((KDE_CHUNKS * csz, nf), 1e15, np.float32)
+    a[:m] = y
+    return a.reshape(-1, 8, nf).transpose(0, 2, 1)
 
 
 def _np(t: torch.Tensor) -> np.ndarray:
@@ -228,6 +254,7 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
         if 1 <= dp <= 3:
             offs["kq"] = blob.add(_kde_pack([_np(pts_p) * c_p]))
             offs["kr"] = blob.add(_kde_pack([_np(pts_p) * c_p], records=True))
+            offs["kv"] = blob.add(_kde_pack_valu(_np(pts_p) * c_p))
         if dp + D <= 3:
             offs["kqy"] = blob.add(_kde_pack(([_np(pts_p) * c_p] if dp else []) + [_np(pts_y) * c_y]))
         stride = dp + D
@@ -326,13 +353,14 @@ def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
 
 def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[str],
                logp: Sequence[str], out_nodes: Sequence[str], shared_roots: bool, mode: int,
-               skip: Sequence[str] = (), exact_f32: bool = False) -> QueryPlan:
+               skip: Sequence[str] = (), exact_f32: bool = False, kde_valu: bool = False) -> QueryPlan:
     """Step table for one query signature.
 
     ``latent``: nodes sampled; ``fixed``: nodes read from the fixed buffer (evidence/do);
     ``logp``: nodes whose log p(value | parents) is accumulated; ``out_nodes``: nodes whose
     values are written per particle; ``skip``: nodes not walked at all; ``exact_f32``: run
-    the MLPs' hidden layer on the exact f32 MFMA chain instead of the split-f16 product.
+    the MLPs' hidden layer on the exact f32 MFMA chain instead of the split-f16 product;
+    ``kde_valu``: KDE pairwise distances on packed VALU instead of the 16x16x4 f32 MFMA tile.
     """
     model = packed.model
     latent_s, fixed_s, logp_s, skip_s = set(latent), set(fixed), set(logp), set(skip)
@@ -403,6 +431,8 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
             fl |= F_SHARED
         if exact_f32:
             fl |= F_F32L2
+        if kde_valu and npk.kind == KIND_ID["kde"]:
+            fl |= F_KDE_VALU
         row[S_FLAGS] = fl
         row[S_ACT] = npk.act
         row[S_NIN] = npk.n_in
@@ -426,6 +456,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         row[S_OFF_KQ] = npk.offs.get("kq", -1)
         row[S_OFF_KQY] = npk.offs.get("kqy", -1)
         row[S_OFF_KR] = npk.offs.get("kr", -1)
+        row[S_OFF_KV] = npk.offs.get("kv", -1)
     out_cols: List[int] = []
     for n in out_nodes:
         out_cols.extend(range(slot_of[n], slot_of[n] + model.out_dim(n)))
