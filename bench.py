@@ -164,8 +164,10 @@ def main():
 
     cfg, g, model, vbn, query = build_workload(args.config, device, rank)
     B, S = cfg["B"], cfg["S"]
+    extra = {"n_particles": S} if cfg["engine"] == "rao_blackwellized_marginalization" else {}
     vbn.set_inference_method(cfg["engine"], n_samples=S, q_base=rank * B,
-                             prune_barren=args.prune_barren, exact_f32=args.exact_f32, kde_valu=args.kde_valu)
+                             prune_barren=args.prune_barren, exact_f32=args.exact_f32, kde_valu=args.kde_valu,
+                             **extra)
     if cfg["engine"] == "importance_sampling":
         vbn._inference._lw.q_base = rank * B
 

@@ -23,6 +23,9 @@
  *                             MDNCPD          (vbn/cpds/mdn.py:185-272)
  *                             KDECPD          (vbn/cpds/kde.py:105-182)
  *                             SoftmaxNNCPD    (vbn/cpds/softmax_nn.py:581-759).
+ *   vbn_hip_rb_epilogue     the Rao-Blackwellized mixture / categorical marginal of
+ *                             RaoBlackwellizedMarginalization.infer_posterior
+ *                               (vbn/inference/rao_blackwellized_marginalization.py:255-317)
  *   vbn_hip_normalize_weights  torch.softmax(log_weights, 1) + ESS
  *                               (importance_sampling.py:82-84) and the normalize / max-shift
  *                               branch of likelihood_weighting.py:75-80.
@@ -36,7 +39,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 2
+#define VBN_ABI_VERSION 3
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001
@@ -52,7 +55,14 @@ enum vbn_kind {
 };
 
 /* role of a node for one query signature */
-enum vbn_role { VBN_ROLE_SKIP = 0, VBN_ROLE_LATENT = 1, VBN_ROLE_FIXED = 2 };
+enum vbn_role {
+  VBN_ROLE_SKIP = 0,
+  VBN_ROLE_LATENT = 1,
+  VBN_ROLE_FIXED = 2,
+  VBN_ROLE_PARAMS = 3   /* write the CPD's conditional parameters, no draw (RB target):
+                           gaussian_nn / linear_gaussian: loc[D] ++ scale[D];
+                           softmax_nn (D = 1): class probabilities[C]                   */
+};
 
 /* step flags */
 #define VBN_F_LOGP 1        /* add log p(value | parents) to the particle's accumulator */
@@ -127,6 +137,20 @@ int vbn_hip_walk(const vbn_walk_args* args, void* stream);
  * log_w and w may alias. */
 int vbn_hip_normalize_weights(const float* log_w, float* w, float* ess, int64_t n_queries,
                               int32_t n_samples, int32_t normalize, float eps, void* stream);
+
+/* Rao-Blackwellized target epilogue over P particles per query
+ * (rao_blackwellized_marginalization.py:68-76, 255-317):
+ *   w = normalized weights of log_w (nan -> -1e30, +-inf -> +-1e30, max-shift, exp, sum;
+ *       uniform 1/P where the sum <= eps)
+ *   mode 0 (gaussian target): params [B][P][2] = (loc, scale); scale sanitized (nan/inf ->
+ *       min_scale, abs, >= min_scale); mixture mean/std; grid[b][s] = lo + (hi - lo) z[s] with
+ *       lo/hi = mean -+ stddevs std; pdf[b][s] = sum_p w_p N(grid; loc_p, scale_p)
+ *   mode 1 (categorical target): params [B][P][C] class probabilities;
+ *       pdf[b][c] = sum_p w_p params[b][p][c]  (n_out = C, grid and z unused)
+ * params may have a batch of 1 (params_b = 1: shared by every query). */
+int vbn_hip_rb_epilogue(const float* log_w, const float* params, int64_t params_b, const float* z,
+                        float* pdf, float* grid, int64_t n_queries, int32_t n_particles, int32_t n_out,
+                        int32_t mode, float stddevs, float min_scale, float eps, void* stream);
 
 /* LDS bytes one 64-particle wave needs for a plan (host helper). */
 int64_t vbn_hip_lds_bytes(int32_t n_slots, int32_t max_out);

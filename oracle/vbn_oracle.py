@@ -641,3 +641,125 @@ def ancestral(model: BNModel, target: Optional[str], evidence: Dict, do: Dict, n
     if target:
         return particles[..., cols[target]]
     return {node: particles[..., cols[node]] for node in model.topo}
+
+
+# ----------------------------------------------------------------------------------------
+# rao_blackwellized_marginalization (reference vbn/inference/rao_blackwellized_marginalization.py)
+# ----------------------------------------------------------------------------------------
+
+def descendants(model: BNModel, node: str) -> set:
+    ch = model.children()
+    out, stack = set(), [node]
+    while stack:
+        for c in ch[stack.pop()]:
+            if c not in out:
+                out.add(c)
+                stack.append(c)
+    return out
+
+
+def rb_normalized_weights(log_w: torch.Tensor, eps: float = 1e-12) -> torch.Tensor:
+    """_normalized_weights (68-76)."""
+    log_w = torch.nan_to_num(log_w, nan=-1e30, posinf=1e30, neginf=-1e30)
+    log_w = log_w - log_w.max(dim=1, keepdim=True).values
+    w = torch.exp(log_w)
+    denom = w.sum(dim=1, keepdim=True)
+    uniform = torch.full_like(w, 1.0 / max(1, w.shape[1]))
+    return torch.where(denom > eps, w / denom.clamp_min(eps), uniform)
+
+
+def _rb_to3d(t: torch.Tensor, b: int):
+    """_to_3d (78-89)."""
+    if t.dim() == 1:
+        t = t.view(1, 1, -1)
+    elif t.dim() == 2:
+        t = t.unsqueeze(1)
+    if t.shape[0] == 1 and b > 1:
+        t = t.expand(b, -1, -1)
+    return t
+
+
+def rao_blackwellized(model: BNModel, target: str, evidence: Dict, do: Dict, n_samples: int,
+                      n_particles: int, draws, stddevs: float = 4.0, min_scale: float = 1e-6):
+    """rao_blackwellized_marginalization.py:196-324.  Returns (pdf, samples, fallback_reason);
+    a reason means the reference hands the query to its fallback engine (pdf/samples None)."""
+    b = _batch(evidence, do)
+    desc = descendants(model, target)
+    if any(x in evidence or x in do for x in desc):                                 # 209-217
+        return None, None, "target has observed/intervened descendants"
+    fixed = _fixed(evidence, do, clamp=True)                                         # 219
+    if target in fixed:                                                              # 220-224
+        return torch.ones(b, 1), fixed[target].unsqueeze(1).expand(b, 1, -1), None
+    cols, total = _layout(model)
+    P = n_particles
+    particles = torch.zeros(b, P, total)
+    log_w = torch.zeros(b, P)
+    for node in model.topo:                                                          # 234-253
+        if node in desc or node == target:
+            continue
+        pt = _gather_parents(model, node, particles, cols)
+        if node in fixed:
+            value = fixed[node].unsqueeze(1).expand(b, P, -1)
+            particles[..., cols[node]] = value
+            if node in evidence:
+                log_w = log_w + cpd_log_prob(model.cpds[node], value, pt)
+            continue
+        particles[..., cols[node]] = cpd_sample(model.cpds[node], pt, P, draws)
+    w = rb_normalized_weights(log_w)                                                  # 255
+    rec = model.cpds[target]
+    pt = _gather_parents(model, target, particles, cols)
+    unsupported = (None, None, "unsupported target CPD for RB marginalization")
+    if rec.kind == "softmax_nn":                                                     # 154-194, 265-280
+        c = int(rec.hp("n_classes"))
+        if pt is None:
+            logits = _smx_root_logits(rec).view(1, 1, rec.output_dim, c).expand(b, 1, -1, -1)
+        else:
+            logits = _smx_logits(rec, pt)
+        probs = torch.softmax(logits, dim=-1)
+        if probs.dim() == 4 and probs.shape[2] == 1:
+            probs = probs[:, :, 0, :]
+        if probs.dim() != 3:
+            return unsupported
+        if probs.shape[1] != P:
+            probs = probs.expand(-1, P, -1)
+        support = rec.state["_sample_values"][0].float()
+        return (w.unsqueeze(-1) * probs).sum(dim=1), support.view(1, -1, 1).expand(b, -1, 1), None
+    if rec.kind == "linear_gaussian":                                                # 100-124
+        if pt is None:
+            loc = rec.state["_bias"].view(1, 1, -1)
+            scale = _lg_scale(rec).view(1, 1, -1)
+        else:
+            loc = pt @ rec.state["_weight"] + rec.state["_bias"]
+            scale = _lg_scale(rec).view(1, 1, -1).expand_as(loc)
+    elif rec.kind == "gaussian_nn":                                                  # 125-130
+        loc, scale = _gnn_root_loc_scale(rec) if pt is None else _gnn_loc_scale(rec, pt)
+    else:
+        return unsupported
+    loc, scale = _rb_to3d(loc, b), _rb_to3d(scale, b)                                 # 136-152
+    if loc.shape[-1] != 1 or scale.shape[-1] != 1:
+        return unsupported
+    if scale.shape[1] == 1 and loc.shape[1] > 1:
+        scale = scale.expand(-1, loc.shape[1], -1)
+    elif loc.shape[1] == 1 and scale.shape[1] > 1:
+        loc = loc.expand(-1, scale.shape[1], -1)
+    scale = torch.nan_to_num(scale, nan=min_scale, posinf=min_scale, neginf=min_scale).abs()
+    scale = scale.clamp_min(min_scale)
+    if loc.shape[1] != P:                                                             # 285-288
+        loc = loc.expand(-1, P, -1)
+        scale = scale.expand(-1, P, -1)
+    comp_var = scale.squeeze(-1) ** 2                                                 # 297-317
+    comp_mean = loc.squeeze(-1)
+    mix_mean = (w * comp_mean).sum(dim=1)
+    second = (w * (comp_var + comp_mean ** 2)).sum(dim=1)
+    mix_var = (second - mix_mean ** 2).clamp_min(min_scale ** 2)
+    mix_std = mix_var.sqrt()
+    z = torch.linspace(0.0, 1.0, n_samples).view(1, n_samples, 1)
+    lo = (mix_mean - stddevs * mix_std).view(b, 1, 1)
+    hi = (mix_mean + stddevs * mix_std).view(b, 1, 1)
+    grid = lo + (hi - lo) * z
+    x = grid.squeeze(-1).unsqueeze(1)
+    mu = loc.squeeze(-1).unsqueeze(-1)
+    sigma = scale.squeeze(-1).unsqueeze(-1).clamp_min(min_scale)
+    z_norm = (x - mu) / sigma
+    comp_pdf = torch.exp(-0.5 * z_norm ** 2) / (math.sqrt(2.0 * math.pi) * sigma)
+    return (w.unsqueeze(-1) * comp_pdf).sum(dim=1), grid, None

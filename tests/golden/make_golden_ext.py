@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""Golden fixtures for the engines past the first round's set (build container only).
+
+Same recorder as ``make_golden.py`` (every RNG call of the reference recorded with its node);
+writes ``tests/golden/ext_*.pt``.  Cases:
+
+* ``rao_blackwellized_marginalization`` (rao_blackwellized_marginalization.py:196-324):
+  gaussian (linear_gaussian, gaussian_nn) and categorical (softmax_nn) targets, root targets,
+  a fixed target, and both fallback reasons (observed descendant, unsupported target CPD);
+  the fallback LW's draws are phase 1 (the unsupported-target case walks its particles first).
+
+Usage: python tests/golden/make_golden_ext.py [--out tests/golden]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import make_golden as G  # noqa: E402
+
+
+def run_rb(vbn, seed, query, n_samples, n_particles):
+    rec = G.Recorder(seed)
+    out = {"engine": "rao_blackwellized_marginalization",
+           "params": {"n_particles": int(n_particles)}, "n_samples": int(n_samples),
+           "query": {"target": query["target"],
+                     "evidence": {k: v.clone() for k, v in query.get("evidence", {}).items()},
+                     "do": {k: v.clone() for k, v in query.get("do", {}).items()}},
+           "seed": seed}
+    G.tag_nodes(vbn, rec)
+    try:
+        with rec:
+            vbn.set_inference_method("rao_blackwellized_marginalization", n_samples=n_samples,
+                                     n_particles=n_particles)
+            fb = vbn._inference._fallback
+            orig = fb.infer_posterior
+
+            def fb_wrapped(*a, _o=orig, **k):          # fallback engine's draws: phase 1
+                rec.phase = 1
+                return _o(*a, **k)
+            fb.infer_posterior = fb_wrapped
+            pdf, samples = vbn.infer_posterior(query)
+            eng = vbn._inference
+            out["outputs"] = {"pdf": pdf.clone(), "samples": samples.clone(),
+                              "fallback": bool(eng._last_fallback),
+                              "reason": str(eng._last_reason or "")}
+    finally:
+        G.untag_nodes(vbn)
+    out["draws"] = rec.records
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=HERE)
+    args = ap.parse_args()
+    if not os.path.isdir(os.path.join(G.REF, "vbn")):
+        print(f"reference not found at {G.REF}; nothing to do")
+        return 0
+    sys.path.insert(0, G.REF)
+    os.environ.setdefault("CI", "1")
+    import networkx as nx
+    import vbn as vbn_mod  # noqa: F401
+    from vectorizedbayesiannetwork_amd import synthetic
+
+    torch.manual_seed(0)
+    fixtures = {}
+
+    # 1) the reference test's linear chain x -> y -> z (tests/test_rao_blackwellized_marginalization.py)
+    g = nx.DiGraph()
+    g.add_edges_from([("x", "y"), ("y", "z")])
+    gen = torch.Generator().manual_seed(0)
+    x = torch.randn(1024, 1, generator=gen)
+    y = 1.2 * x + 0.3 + 0.2 * torch.randn(1024, 1, generator=gen)
+    z = -0.7 * y + 0.1 + 0.2 * torch.randn(1024, 1, generator=gen)
+    data = {"x": x, "y": y, "z": z}
+    vbn = G.fit_model(vbn_mod, g, {n: "linear_gaussian" for n in g.nodes}, data)
+    rows = torch.arange(3) * 5 + 1
+    cases = [
+        run_rb(vbn, 11, {"target": "y", "evidence": {"x": x[rows]}}, 9, 16),
+        run_rb(vbn, 12, {"target": "z", "evidence": {"x": x[rows]}}, 7, 32),           # y marginalised
+        run_rb(vbn, 13, {"target": "x", "evidence": {}}, 5, 8),                         # root target
+        run_rb(vbn, 14, {"target": "y", "evidence": {"z": z[rows]}}, 9, 16),           # observed descendant
+        run_rb(vbn, 15, {"target": "y", "evidence": {"y": y[rows], "x": x[rows]}}, 6, 8),  # fixed target
+    ]
+    fixtures["ext_rb_chain"] = {"model": G.checkpoint_dict(vbn), "cases": cases}
+
+    # 2) 10-node random DAG, gaussian_nn / softmax_nn / linear_gaussian / mdn round robin
+    g10 = synthetic.random_dag(10, seed=7)
+    d10 = synthetic.sem_data(g10, 512, seed=0)
+    kinds = synthetic.round_robin_kinds(g10, ["gaussian_nn", "softmax_nn", "linear_gaussian", "mdn"])
+    vbn = G.fit_model(vbn_mod, g10, kinds, d10)
+    topo = list(nx.topological_sort(g10))
+    rows = torch.arange(4) * 9 + 2
+    cases = []
+    s = 100
+    for node in topo:
+        desc = nx.descendants(g10, node)
+        anc = [a for a in topo if a not in desc and a != node]
+        ev_nodes = anc[-3:] if len(anc) >= 3 else anc
+        q = {"target": node, "evidence": {a: d10[a][rows] for a in ev_nodes}}
+        cases.append(run_rb(vbn, s, q, 11, 24))
+        s += 1
+    fixtures["ext_rb_mix10"] = {"model": G.checkpoint_dict(vbn), "cases": cases}
+
+    os.makedirs(args.out, exist_ok=True)
+    for name, fx in fixtures.items():
+        path = os.path.join(args.out, f"{name}.pt")
+        torch.save(fx, path)
+        torch.load(path, weights_only=True)
+        print(f"{name}: {len(fx['cases'])} cases -> {path} ({os.path.getsize(path) / 1024:.1f} KiB)")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

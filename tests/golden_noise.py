@@ -14,6 +14,8 @@ import torch
 
 def noise_dict(case: dict, model, phase: int = 0) -> Dict[str, Tuple[torch.Tensor, torch.Tensor]]:
     S = int(case["n_samples"])
+    if case["engine"] == "rao_blackwellized_marginalization" and phase == 0:
+        S = int(case["params"]["n_particles"])        # the RB walk runs over the particles
     slots: Dict[str, Dict[int, list]] = {}
     for r in case["draws"]:
         if r["phase"] != phase:

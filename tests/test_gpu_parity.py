@@ -115,6 +115,18 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
         xs = AncestralSampler(n_samples=n, kde_valu=kde_valu).sample(vbn, qq, n, _noise=nd0)
         rxs = O.ancestral(model, q["target"], q["evidence"], q["do"], n, draws)
         _close("samples", xs, rxs, S_ATOL, S_RTOL)
+    elif eng == "rao_blackwellized_marginalization":
+        from vectorizedbayesiannetwork_amd.engines import RaoBlackwellizedMarginalization
+        e = RaoBlackwellizedMarginalization(n_samples=n, n_particles=p["n_particles"], kde_valu=kde_valu)
+        pdf, xs = e.infer_posterior(vbn, qq, _noise=nd0, _noise_fallback=noise_dict(case, model, 1))
+        rpdf, rxs, reason = O.rao_blackwellized(model, q["target"], q["evidence"], q["do"], n,
+                                                p["n_particles"], draws)
+        if reason:
+            rpdf, rxs = O.likelihood_weighting(model, q["target"], q["evidence"], q["do"], n, draws)
+        assert e._last_fallback == bool(reason) == case["outputs"]["fallback"]
+        assert (e._last_reason or "") == (reason or "")
+        _close("samples", xs, rxs, S_ATOL, S_RTOL)
+        _close("pdf", pdf, rpdf, P_ATOL, P_RTOL)
     else:
         raise AssertionError(eng)
 

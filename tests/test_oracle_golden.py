@@ -31,6 +31,12 @@ def _run_case(model, case):
         out = {"pdf": w, "samples": xs, "ess": ess, "fallback": fb}
     elif eng == "ancestral":
         out = {"samples": O.ancestral(model, q["target"], q["evidence"], q["do"], n, draws)}
+    elif eng == "rao_blackwellized_marginalization":
+        pdf, xs, reason = O.rao_blackwellized(model, q["target"], q["evidence"], q["do"], n,
+                                              p["n_particles"], draws)
+        if reason:                               # fallback engine: likelihood_weighting
+            pdf, xs = O.likelihood_weighting(model, q["target"], q["evidence"], q["do"], n, draws)
+        out = {"pdf": pdf, "samples": xs, "fallback": bool(reason), "reason": reason or ""}
     else:
         raise AssertionError(eng)
     assert draws.exhausted(), "oracle consumed fewer draws than the reference"
@@ -38,7 +44,7 @@ def _run_case(model, case):
 
 
 def _eq(a, b):
-    if isinstance(a, bool):
+    if isinstance(a, (bool, str)):
         return a == b
     return a.shape == b.shape and torch.equal(torch.nan_to_num(a, nan=123.0), torch.nan_to_num(b, nan=123.0)) \
         and torch.equal(a.isnan(), b.isnan())

@@ -202,3 +202,78 @@ def test_bench_configs_pack(cfg):
     _check_liveness(model, plan)
     assert plan.n_slots < len(model.topo)               # liveness reuses slots
     assert (plan.steps[:, S_ROLE] == ROLE_FIXED).sum() == len(ev)
+
+
+def test_rb_params_plan_roles_and_widths():
+    """RB target walks as role PARAMS with loc++scale (gaussian) or C probabilities (softmax_nn)."""
+    from vectorizedbayesiannetwork_amd.plan import ROLE_PARAMS, S_KIND
+    model = model_from_checkpoint(load_golden("ext_rb_mix10")["model"])
+    pk = PackedModel(model, torch.device("cpu"))
+    seen = set()
+    for target in model.topo:
+        rec = model.cpds[target]
+        if rec.kind not in ("gaussian_nn", "linear_gaussian", "softmax_nn"):
+            continue
+        desc, stack = set(), [target]
+        ch = model.children()
+        while stack:
+            for c in ch[stack.pop()]:
+                if c not in desc:
+                    desc.add(c)
+                    stack.append(c)
+        keep = [x for x in model.topo if x not in desc]
+        ev = [x for x in keep if x != target][:2]
+        plan = build_plan(pk, latent=[x for x in keep if x not in ev and x != target], fixed=ev, logp=ev,
+                          out_nodes=[target], params=[target], shared_roots=True, mode=MODE_WEIGHTED,
+                          skip=sorted(desc))
+        row = [r for r in plan.steps.tolist() if r[S_OUTCOL] == plan.slot_of[target] and r[S_ROLE] == ROLE_PARAMS]
+        assert len(row) == 1
+        width = 2 if rec.kind != "softmax_nn" else int(rec.hp("n_classes"))
+        assert plan.out_cols.numel() == width
+        assert plan.out_cols.tolist() == list(range(plan.slot_of[target], plan.slot_of[target] + width))
+        seen.add(rec.kind)
+    assert seen == {"gaussian_nn", "linear_gaussian", "softmax_nn"}
+
+
+def _mfma_16x16x4(a_lane, b_lane, c_lane):
+    """v_mfma_f32_16x16x4_f32: A[l&15][l>>4], B[l>>4][l&15]; D lane l rows 4(l>>4)+r, col l&15."""
+    A = np.zeros((16, 4)); B = np.zeros((4, 16))
+    for l in range(64):
+        A[l & 15, l >> 4] = a_lane[l]
+        B[l >> 4, l & 15] = b_lane[l]
+    D = A @ B
+    return np.array([[D[4 * (l >> 4) + r, l & 15] + c_lane[l][r] for r in range(4)] for l in range(64)])
+
+
+@pytest.mark.parametrize("nf", [1, 2, 3])
+def test_kde_mfma_pack_gives_kernel_weights(nf):
+    """The KDE point packs (plan._kde_pack) in the 16x16x4 operand layout, with the particle
+    operands of csrc kde_operands (zero-C form for nf <= 2, C = -|x'|^2 for nf = 3), give
+    exp2(D) = exp(-|x - y|^2 / (2 s^2)) for every (particle, point); padding points weigh 0."""
+    from vectorizedbayesiannetwork_amd.plan import _KDE_C, _kde_cb, _kde_pack, KDE_CHUNKS
+    rng = np.random.default_rng(nf)
+    m, s = 37, 0.7
+    c = np.float32(_KDE_C / s)
+    pts = rng.normal(size=(m, nf)).astype(np.float32)
+    parts = rng.normal(size=(64, nf)).astype(np.float32)
+    pack = _kde_pack([pts * c])                                 # [blocks][4][16]
+    assert pack.shape == (KDE_CHUNKS * _kde_cb(m), 4, 16)
+    xv = parts * c
+    w = np.zeros((64, pack.shape[0] * 16))
+    for t in range(4):
+        b_lane, c_lane = np.zeros(64), np.zeros((64, 4))
+        for l in range(64):
+            g, n = l >> 4, l & 15
+            x = xv[16 * t + n].astype(np.float64)
+            sq = float((x ** 2).sum())
+            b_lane[l] = 2 * x[g] if g < nf else (-1.0 if g == nf else (-sq if (g == nf + 1 and nf <= 2) else 0.0))
+            c_lane[l] = 0.0 if nf <= 2 else -sq
+        for blk in range(pack.shape[0]):
+            a_lane = pack[blk].reshape(-1)                      # lane l reads element blk*64 + l
+            d = _mfma_16x16x4(a_lane, b_lane, c_lane)
+            for l in range(64):
+                for r in range(4):
+                    w[16 * t + (l & 15), blk * 16 + 4 * (l >> 4) + r] = np.exp2(d[l, r])
+    ref = np.exp(-0.5 * ((parts[:, None, :].astype(np.float64) - pts[None].astype(np.float64)) ** 2).sum(-1) / s ** 2)
+    np.testing.assert_allclose(w[:, :m], ref, rtol=1e-5, atol=1e-30)
+    assert (w[:, m:] == 0).all()

@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -20,6 +20,7 @@ EXPORTS = (
     "vbn_hip_last_error",
     "vbn_hip_walk",
     "vbn_hip_normalize_weights",
+    "vbn_hip_rb_epilogue",
     "vbn_hip_lds_bytes",
     "vbn_hip_struct_size",
 )
@@ -89,6 +90,11 @@ def load(path: str = None) -> ctypes.CDLL:
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
             ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
         lib.vbn_hip_normalize_weights.restype = ctypes.c_int
+        lib.vbn_hip_rb_epilogue.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+            ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_void_p]
+        lib.vbn_hip_rb_epilogue.restype = ctypes.c_int
         lib.vbn_hip_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
         lib.vbn_hip_lds_bytes.restype = ctypes.c_int64
         lib.vbn_hip_struct_size.argtypes = [ctypes.c_int]

@@ -36,6 +36,8 @@ _ENGINE_DEFAULTS = {
         "monte_carlo_marginalization": {"n_samples": 1024},
         "importance_sampling": {"n_samples": 1024},
         "likelihood_weighting": {"n_samples": 1024, "eps": 1e-12, "normalize": True},
+        "rao_blackwellized_marginalization": {"n_samples": 256, "n_particles": 256, "stddevs": 4.0,
+                                              "min_scale": 1e-6, "fallback": "likelihood_weighting"},
     },
     "sampling": {"ancestral": {"n_samples": 512}},
 }

@@ -408,6 +408,11 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
   if (st.flags & VBN_F_ROOT) {
     for (int d = 0; d < D; ++d) {
       const float loc = t[d], scale = t[D + d];
+      if (st.role == VBN_ROLE_PARAMS) {
+        vwrite(L, st.out_col + d, loc);
+        vwrite(L, st.out_col + D + d, scale);
+        continue;
+      }
       float x;
       if (latent) {
         x = draw_normal(A, st, d, L) * scale + loc;  // torch.normal(loc, scale)
@@ -432,6 +437,11 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
     const float sy = t[d], my = t[D + d];
     const float loc = o_loc * sy + my;
     const float scale = (softplus_t(o_sc) + min_scale) * sy;
+    if (st.role == VBN_ROLE_PARAMS) {
+      vwrite(L, st.out_col + d, loc);
+      vwrite(L, st.out_col + D + d, scale);
+      continue;
+    }
     float x;
     if (latent) {
       x = loc + draw_normal(A, st, d, L) * scale;
@@ -466,6 +476,11 @@ __device__ __forceinline__ void step_linear_gaussian(const vbn_walk_args& A, con
     float mu = 0.f;
     for (int i = 0; i < nin; ++i) mu = fmaf(vread(L, L.ic[st.in_off + i]), W[d * nin + i], mu);
     const float loc = (nin > 0) ? mu + bias[d] : bias[d];
+    if (st.role == VBN_ROLE_PARAMS) {
+      vwrite(L, st.out_col + d, loc);
+      vwrite(L, st.out_col + D + d, scale[d]);
+      continue;
+    }
     float x;
     if (latent) {
       x = loc + draw_normal(A, st, d, L) * scale[d];
@@ -610,6 +625,10 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
     for (int c = 0; c < C; ++c) m = fmaxf(m, logit(c));
     float se = 0.f;
     for (int c = 0; c < C; ++c) se += __expf(logit(c) - m);
+    if (st.role == VBN_ROLE_PARAMS) {                   // softmax(logits) (RB target, D = 1)
+      for (int c = 0; c < C; ++c) vwrite(L, st.out_col + c, __expf(logit(c) - m) / se);
+      return;
+    }
     const bool disc = (st.aux1 >> d) & 1;
     const float* e = edges + d * (C + 1);
     float x;
@@ -1349,6 +1368,110 @@ __global__ void __launch_bounds__(NW_THREADS) vbn_normalize_kernel(const float* 
 }
 
 // ------------------------------------------------------------------------------------------
+// Rao-Blackwellized epilogue (rao_blackwellized_marginalization.py:68-76, 255-317): one
+// 256-thread workgroup per query; weights / component parameters staged in LDS, the mixture
+// density evaluated with one grid point per thread (the component loop reads LDS broadcasts).
+// ------------------------------------------------------------------------------------------
+#define RB_THREADS 256
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int k = 0; k < RB_THREADS / WAVE; ++k) t += red[k];
+  return t;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = red[0];
+  for (int k = 1; k < RB_THREADS / WAVE; ++k) t = fmaxf(t, red[k]);
+  return t;
+}
+
+__global__ void __launch_bounds__(RB_THREADS) vbn_rb_epilogue_kernel(
+    const float* __restrict__ log_w, const float* __restrict__ params, int64_t params_b,
+    const float* __restrict__ z, float* __restrict__ pdf, float* __restrict__ grid, int P, int n_out,
+    int mode, float stddevs, float min_scale, float eps) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ float red[RB_THREADS / WAVE];
+  float* w = sm;            // [P]
+  float* mu = sm + P;       // [P]   (gaussian)
+  float* inv = sm + 2 * P;  // [P]   1/sigma
+  float* cf = sm + 3 * P;   // [P]   w / (sqrt(2 pi) sigma)
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* lw = log_w + b * P;
+  const float* prm = params + (params_b == 1 ? 0 : b) * (int64_t)P * (mode == 0 ? 2 : n_out);
+  // _normalized_weights (68-76)
+  float m = -INFINITY;
+  for (int p = tid; p < P; p += RB_THREADS) {
+    float v = lw[p];
+    v = (v != v) ? -1e30f : (v == INFINITY ? 1e30f : (v == -INFINITY ? -1e30f : v));
+    w[p] = v;
+    m = fmaxf(m, v);
+  }
+  m = block_max(m, red);
+  float s = 0.f;
+  for (int p = tid; p < P; p += RB_THREADS) {
+    const float e = expf(w[p] - m);
+    w[p] = e;
+    s += e;
+  }
+  const float denom = block_sum(s, red);
+  const bool ok = denom > eps;
+  const float dn = fmaxf(denom, eps), uni = 1.0f / (float)max(1, P);
+  for (int p = tid; p < P; p += RB_THREADS) w[p] = ok ? w[p] / dn : uni;
+  __syncthreads();
+  if (mode == 1) {                                        // categorical (278)
+    for (int c = 0; c < n_out; ++c) {
+      float acc = 0.f;
+      for (int p = tid; p < P; p += RB_THREADS) acc += w[p] * prm[(int64_t)p * n_out + c];
+      const float t = block_sum(acc, red);
+      if (tid == 0) pdf[b * n_out + c] = t;
+    }
+    return;
+  }
+  // gaussian mixture (297-317)
+  float a1 = 0.f, a2 = 0.f;
+  for (int p = tid; p < P; p += RB_THREADS) {
+    const float loc = prm[2 * (int64_t)p];
+    float sc = prm[2 * (int64_t)p + 1];
+    sc = (sc != sc || sc == INFINITY || sc == -INFINITY) ? min_scale : fabsf(sc);
+    sc = fmaxf(sc, min_scale);
+    mu[p] = loc;
+    inv[p] = 1.0f / sc;
+    cf[p] = w[p] / (2.5066282746310002f * sc);
+    a1 += w[p] * loc;
+    a2 += w[p] * (sc * sc + loc * loc);
+  }
+  const float mean = block_sum(a1, red);
+  const float second = block_sum(a2, red);
+  const float var = fmaxf(second - mean * mean, min_scale * min_scale);
+  const float sd = sqrtf(var);
+  const float lo = mean - stddevs * sd, hi = mean + stddevs * sd;
+  __syncthreads();
+  for (int j = tid; j < n_out; j += RB_THREADS) {
+    const float x = lo + (hi - lo) * z[j];
+    float acc = 0.f;
+    for (int p = 0; p < P; ++p) {
+      const float zn = (x - mu[p]) * inv[p];
+      acc = fmaf(cf[p], __expf(-0.5f * (zn * zn)), acc);
+    }
+    pdf[b * n_out + j] = acc;
+    grid[b * n_out + j] = x;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // C-ABI
 // ------------------------------------------------------------------------------------------
 static thread_local char g_err[512];
@@ -1400,6 +1523,22 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
     case 31u: hipLaunchKernelGGL(vbn_walk_kernel<31u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
     default: hipLaunchKernelGGL(vbn_walk_kernel<63u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
   }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  return 0;
+}
+
+extern "C" int vbn_hip_rb_epilogue(const float* log_w, const float* params, int64_t params_b, const float* z,
+                                   float* pdf, float* grid, int64_t n_queries, int32_t n_particles, int32_t n_out,
+                                   int32_t mode, float stddevs, float min_scale, float eps, void* stream) {
+  if (!log_w || !params || !pdf || n_queries <= 0 || n_particles <= 0 || n_out <= 0 || (mode != 0 && mode != 1) ||
+      (mode == 0 && (!z || !grid)) || (params_b != 1 && params_b != n_queries))
+    return fail(VBN_E_ARGS, "vbn_hip_rb_epilogue: bad arguments");
+  const size_t lds = (size_t)n_particles * 4 * sizeof(float);
+  if (lds > 64 * 1024) return fail(VBN_E_LDS, "vbn_hip_rb_epilogue: more than 4096 particles per query");
+  hipLaunchKernelGGL(vbn_rb_epilogue_kernel, dim3((unsigned)n_queries), dim3(RB_THREADS), lds,
+                     (hipStream_t)stream, log_w, params, params_b, z, pdf, grid, n_particles, n_out, mode,
+                     stddevs, min_scale, eps);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;

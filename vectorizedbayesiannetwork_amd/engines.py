@@ -17,6 +17,10 @@ Semantics mirror the reference branch by branch:
 * LW (likelihood_weighting.py:24-82): evidence clamped (nan->0, +-1e6), shared root draws,
   softmax or max-shifted exp.
 * ancestral (sampling/ancestral.py:13-65): the walk without weights; target slice or all nodes.
+* RB (rao_blackwellized_marginalization.py:196-324): LW-style walk over the target's
+  non-descendants with the target written as its conditional parameters, then one epilogue
+  launch (weights, mixture moments, grid density / categorical marginal); fallback engine for
+  observed descendants and unsupported target CPDs.
 
 RNG: counter-based Philox keyed by ``(seed, offset, node, query, sample)``.  The seed of a
 call is taken from the global torch generator (so ``torch.manual_seed`` makes runs
@@ -42,6 +46,7 @@ __all__ = [
     "ImportanceSampling",
     "LikelihoodWeighting",
     "AncestralSampler",
+    "RaoBlackwellizedMarginalization",
     "infer_batch_size",
 ]
 
@@ -352,6 +357,99 @@ class ImportanceSampling(LikelihoodWeighting):
                                             _noise=kwargs.get("_noise_fallback"))
         self._last_fallback = False
         return w, xs
+
+
+def _descendants(model: BNModel, node: str) -> set:
+    ch = model.children()
+    out, stack = set(), [node]
+    while stack:
+        for c in ch[stack.pop()]:
+            if c not in out:
+                out.add(c)
+                stack.append(c)
+    return out
+
+
+@register_inference("rao_blackwellized_marginalization")
+class RaoBlackwellizedMarginalization(_EngineBase):
+    """rao_blackwellized_marginalization.py:15-324 on the GPU."""
+
+    _BASE_KW = ("seed", "prune_barren", "q_base", "exact_f32", "kde_valu")
+
+    def __init__(self, n_samples: int = 200, n_particles: Optional[int] = None, stddevs: float = 4.0,
+                 min_scale: float = 1e-6, fallback: Optional[str] = "likelihood_weighting", **kwargs):
+        super().__init__(n_samples=n_samples, **{k: kwargs[k] for k in self._BASE_KW if k in kwargs})
+        self.n_particles = int(n_particles) if n_particles is not None else self.n_samples
+        self.stddevs = float(stddevs)
+        self.min_scale = float(min_scale)
+        self.fallback = str(fallback).strip().lower() if fallback is not None else "none"
+        self._fallback = None
+        self._last_fallback = False
+        self._last_reason: Optional[str] = None
+        if self.fallback != "none":
+            from .registry import INFERENCE_REGISTRY
+            if self.fallback not in INFERENCE_REGISTRY:
+                raise ValueError(
+                    f"Unknown fallback inference '{fallback}'. Available: {list(INFERENCE_REGISTRY.keys())}")
+            if self.fallback == "rao_blackwellized_marginalization":
+                raise ValueError("fallback cannot be 'rao_blackwellized_marginalization'")
+            fk = dict(kwargs)
+            fk.setdefault("n_samples", self.n_samples)
+            self._fallback = INFERENCE_REGISTRY[self.fallback](**fk)
+
+    def _fallback_infer(self, vbn, query, *, reason: str, **kwargs):
+        self._last_fallback = True
+        self._last_reason = reason
+        if self._fallback is None:
+            raise RuntimeError("rao_blackwellized_marginalization cannot handle this query and has no fallback")
+        kw = {k: v for k, v in kwargs.items() if k not in ("n_particles", "_noise")}
+        if "_noise_fallback" in kw:
+            kw["_noise"] = kw.pop("_noise_fallback")
+        return self._fallback.infer_posterior(vbn, query, **kw)
+
+    def infer_posterior(self, vbn, query, **kwargs):
+        self._last_fallback = False
+        self._last_reason = None
+        n = max(1, int(kwargs.get("n_samples", self.n_samples)))
+        n_part = max(1, int(kwargs.get("n_particles", self.n_particles)))
+        target, ev, do = self._query(query)
+        b = infer_batch_size(ev, do)
+        dev = _device_of(vbn)
+        pk = packed_model(vbn, dev)
+        model = pk.model
+        desc = _descendants(model, target)
+        if any(x in ev or x in do for x in desc):                                   # 209-217
+            return self._fallback_infer(vbn, query, reason="target has observed/intervened descendants", **kwargs)
+        vals = _fixed_values(query, dev, clamp=True)                                 # 219
+        if target in vals:                                                           # 220-224
+            return (torch.ones(b, 1, device=dev, dtype=torch.float32),
+                    vals[target].unsqueeze(1).expand(b, 1, -1))
+        rec = model.cpds[target]
+        if rec.kind == "softmax_nn" and model.out_dim(target) == 1:
+            mode = 1
+        elif rec.kind in ("gaussian_nn", "linear_gaussian") and model.out_dim(target) == 1:
+            mode = 0
+        else:
+            return self._fallback_infer(vbn, query, reason="unsupported target CPD for RB marginalization",
+                                        **kwargs)
+        _check_discrete(pk, vals, list(ev))
+        keep = [x for x in model.topo if x not in desc]
+        key = ("rb", target, tuple(sorted(ev)), tuple(sorted(do)))
+        plan = self._plan(pk, key, latent=[x for x in keep if x not in vals and x != target],
+                          fixed=[x for x in keep if x in vals], logp=[x for x in keep if x in ev],
+                          out_nodes=[target], params=[target], shared_roots=True, mode=MODE_WEIGHTED,
+                          skip=sorted(desc))
+        fx = _fixed_buffer(plan, vals, b, dev)
+        log_w, prm = run_walk(pk, plan, fx, b, n_part, seed=self._seed(kwargs), q_base=self.q_base,
+                              noise=kwargs.get("_noise"))
+        if mode == 0:
+            z = torch.linspace(0.0, 1.0, n).to(dev)                                   # 304
+            pdf, grid = ops.rb_epilogue(log_w, prm, z, n, 0, self.stddevs, self.min_scale, 1e-12)
+            return pdf, grid.unsqueeze(-1)
+        c = int(rec.hp("n_classes"))
+        pdf, _ = ops.rb_epilogue(log_w, prm, log_w.new_empty(0), c, 1, self.stddevs, self.min_scale, 1e-12)
+        support = rec.state["_sample_values"][0].to(device=dev, dtype=torch.float32)
+        return pdf, support.view(1, -1, 1).expand(b, -1, 1)
 
 
 @register_sampling("ancestral")

@@ -2,6 +2,7 @@
 
 * ``vbn_hip::walk``               -> ``vbn_hip_walk``             (particle pass)
 * ``vbn_hip::normalize_weights``  -> ``vbn_hip_normalize_weights`` (softmax over S + ESS)
+* ``vbn_hip::rb_epilogue``        -> ``vbn_hip_rb_epilogue``       (Rao-Blackwellized target)
 
 Both run asynchronously on the current HIP stream, allocate fresh contiguous outputs and
 have fake (meta) implementations for shape inference.  Host-side checks make sure every
@@ -18,7 +19,7 @@ from torch import Tensor
 from . import _lib
 from .plan import STEP_INTS
 
-__all__ = ["walk", "normalize_weights"]
+__all__ = ["walk", "normalize_weights", "rb_epilogue"]
 
 
 def _ptr(t: Optional[Tensor]) -> Optional[int]:
@@ -122,3 +123,37 @@ def normalize_weights(log_w: Tensor, normalize: bool, eps: float) -> Tuple[Tenso
 @normalize_weights.register_fake
 def _normalize_fake(log_w, normalize, eps):
     return torch.empty_like(log_w), log_w.new_empty(log_w.shape[0])
+
+
+@torch.library.custom_op("vbn_hip::rb_epilogue", mutates_args=())
+def rb_epilogue(log_w: Tensor, params: Tensor, z: Tensor, n_out: int, mode: int, stddevs: float,
+                min_scale: float, eps: float) -> Tuple[Tensor, Tensor]:
+    """log_w [B,P]; params [B|1, P, 2] (mode 0: loc, scale) or [B|1, P, C] (mode 1: probs);
+    z [n_out] grid fractions (mode 0).  Returns (pdf [B, n_out], grid [B, n_out])."""
+    if log_w.device.type != "cuda" or log_w.dtype != torch.float32 or log_w.dim() != 2:
+        raise ValueError("vbn_hip::rb_epilogue: log_w must be a float32 [B,P] GPU tensor")
+    b, p = log_w.shape
+    width = 2 if mode == 0 else n_out
+    if params.dim() != 3 or params.shape[1] != p or params.shape[2] != width or params.shape[0] not in (1, b):
+        raise ValueError(f"vbn_hip::rb_epilogue: params must be [B|1, {p}, {width}], got {tuple(params.shape)}")
+    log_w = log_w.contiguous()
+    params = params.to(torch.float32).contiguous()
+    if mode == 0:
+        z = z.to(device=log_w.device, dtype=torch.float32).contiguous()
+        if z.numel() != n_out:
+            raise ValueError("vbn_hip::rb_epilogue: z must have n_out values")
+    pdf = torch.empty(b, n_out, device=log_w.device, dtype=torch.float32)
+    grid = torch.empty(b, n_out, device=log_w.device, dtype=torch.float32) if mode == 0 else pdf.new_empty(0)
+    lib = _lib.load()
+    with torch.cuda.device(log_w.device):
+        _lib.check(lib.vbn_hip_rb_epilogue(
+            _ptr(log_w), _ptr(params), params.shape[0], _ptr(z) if mode == 0 else None, _ptr(pdf),
+            _ptr(grid), b, p, n_out, mode, float(stddevs), float(min_scale), float(eps),
+            ctypes.c_void_p(_stream_handle(log_w.device))), "vbn_hip_rb_epilogue")
+    return pdf, grid
+
+
+@rb_epilogue.register_fake
+def _rb_fake(log_w, params, z, n_out, mode, stddevs, min_scale, eps):
+    b = log_w.shape[0]
+    return log_w.new_empty(b, n_out), log_w.new_empty((b, n_out) if mode == 0 else (0,))

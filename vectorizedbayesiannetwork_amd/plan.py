@@ -28,7 +28,7 @@ from .model import BNModel, CPDRecord
 
 # ---- must match include/vbn_hip.h -------------------------------------------------------
 KIND_ID = {"gaussian_nn": 0, "linear_gaussian": 1, "mdn": 2, "kde": 3, "softmax_nn": 4}
-ROLE_SKIP, ROLE_LATENT, ROLE_FIXED = 0, 1, 2
+ROLE_SKIP, ROLE_LATENT, ROLE_FIXED, ROLE_PARAMS = 0, 1, 2, 3
 F_LOGP, F_ROOT, F_SHARED, F_STANDARDIZE, F_CLIP, F_F32L2, F_KDE_VALU = 1, 2, 4, 8, 16, 32, 64
 ACT_ID = {"relu": 0, "tanh": 1, "gelu": 2, "elu": 3}
 WITHIN_ID = {"uniform": 0, "triangular": 1, "gaussian": 2}
@@ -353,7 +353,8 @@ def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
 
 def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[str],
                logp: Sequence[str], out_nodes: Sequence[str], shared_roots: bool, mode: int,
-               skip: Sequence[str] = (), exact_f32: bool = False, kde_valu: bool = False) -> QueryPlan:
+               skip: Sequence[str] = (), exact_f32: bool = False, kde_valu: bool = False,
+               params: Sequence[str] = ()) -> QueryPlan:
     """Step table for one query signature.
 
     ``latent``: nodes sampled; ``fixed``: nodes read from the fixed buffer (evidence/do);
@@ -361,18 +362,36 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
     values are written per particle; ``skip``: nodes not walked at all; ``exact_f32``: run
     the MLPs' hidden layer on the exact f32 MFMA chain instead of the split-f16 product;
     ``kde_valu``: KDE pairwise distances on packed VALU instead of the 16x16x4 f32 MFMA tile.
+    ``params``: nodes whose conditional parameters are written instead of a draw (role
+    PARAMS; gaussian_nn / linear_gaussian: loc ++ scale, softmax_nn with D = 1: class
+    probabilities) -- the Rao-Blackwellized target.
     """
     model = packed.model
     latent_s, fixed_s, logp_s, skip_s = set(latent), set(fixed), set(logp), set(skip)
+    params_s = set(params)
     order = [n for n in model.topo if n not in skip_s]
     for n in order:
+        if n in params_s:
+            if n in latent_s or n in fixed_s or n in logp_s:
+                raise ValueError(f"params node {n} cannot be latent/fixed/logp")
+            continue
         if (n in latent_s) == (n in fixed_s):
             raise ValueError(f"node {n} must be exactly one of latent/fixed")
+
+    def width(n: str) -> int:
+        if n not in params_s:
+            return model.out_dim(n)
+        rec = model.cpds[n]
+        if rec.kind in ("gaussian_nn", "linear_gaussian"):
+            return 2 * model.out_dim(n)
+        if rec.kind == "softmax_nn" and model.out_dim(n) == 1:
+            return int(rec.hp("n_classes"))
+        raise ValueError(f"no parameter output for {rec.kind} node {n} with {model.out_dim(n)} dims")
     # liveness: last step index reading each node's columns
     pos = {n: i for i, n in enumerate(order)}
     last = {n: pos[n] for n in order}
     # a fixed node without log-prob only loads its value: it reads no parents
-    reads = {n: (n in latent_s or n in logp_s) for n in order}
+    reads = {n: (n in latent_s or n in logp_s or n in params_s) for n in order}
     for n in order:
         if not reads[n]:
             continue
@@ -387,7 +406,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
     slot_of: Dict[str, int] = {}
     release: Dict[int, List[str]] = {}
     for i, n in enumerate(order):
-        d = model.out_dim(n)
+        d = width(n)
         # contiguous run of d slots: take from the free list if a run exists
         base = None
         if d == 1 and free:
@@ -408,7 +427,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         release.setdefault(last[n], []).append(n)
         for m in release.pop(i, []):
             if m != n or last[n] == i:
-                free.extend(range(slot_of[m], slot_of[m] + model.out_dim(m)))
+                free.extend(range(slot_of[m], slot_of[m] + width(m)))
     fixed_nodes = [n for n in order if n in fixed_s]
     fixed_col = {}
     c = 0
@@ -423,7 +442,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         npk = packed.nodes[n]
         row = steps[i]
         row[S_KIND] = npk.kind
-        row[S_ROLE] = ROLE_LATENT if n in latent_s else ROLE_FIXED
+        row[S_ROLE] = ROLE_PARAMS if n in params_s else (ROLE_LATENT if n in latent_s else ROLE_FIXED)
         fl = npk.flags
         if n in logp_s:
             fl |= F_LOGP
@@ -459,7 +478,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         row[S_OFF_KV] = npk.offs.get("kv", -1)
     out_cols: List[int] = []
     for n in out_nodes:
-        out_cols.extend(range(slot_of[n], slot_of[n] + model.out_dim(n)))
+        out_cols.extend(range(slot_of[n], slot_of[n] + width(n)))
     dev = packed.device
 
     def t(a):
@@ -468,7 +487,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
 
     kind_mask = 0
     for n in order:
-        if n in latent_s or n in logp_s:
+        if n in latent_s or n in logp_s or n in params_s:
             npk = packed.nodes[n]
             kind_mask |= 1 << npk.kind
             if npk.n_out and npk.act != ACT_ID["relu"]:

@@ -78,6 +78,9 @@ CONFIGS = {
                  kinds=("gaussian_nn", "linear_gaussian", "mdn", "kde", "softmax_nn"),
                  engine="monte_carlo_marginalization", B=65536, S=2048, rows=8192,
                  kde_max_points=4096),
+    # §8(f) row on the cfg2 DAG: Rao-Blackwellized target (P = S = 1024)
+    "rb32": dict(name="32node-gaussian_nn-rb", n_nodes=32, kinds=("gaussian_nn",),
+                 engine="rao_blackwellized_marginalization", B=4096, S=1024, rows=2048),
     "anchor64": dict(name="64node-gaussian_nn-mcm", n_nodes=64, kinds=("gaussian_nn",),
                      engine="monte_carlo_marginalization", B=4096, S=1024, rows=2048),
 }
