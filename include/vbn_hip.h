@@ -23,6 +23,9 @@
  *                             MDNCPD          (vbn/cpds/mdn.py:185-272)
  *                             KDECPD          (vbn/cpds/kde.py:105-182)
  *                             SoftmaxNNCPD    (vbn/cpds/softmax_nn.py:581-759).
+ *   vbn_hip_resample        the multinomial resampling step of
+ *                             ResampledImportanceSampling._resample
+ *                               (vbn/inference/resampled_importance_sampling.py:33-41)
  *   vbn_hip_rb_epilogue     the Rao-Blackwellized mixture / categorical marginal of
  *                             RaoBlackwellizedMarginalization.infer_posterior
  *                               (vbn/inference/rao_blackwellized_marginalization.py:255-317)
@@ -121,6 +124,12 @@ typedef struct vbn_walk_args {
   int64_t q_base;          /* global index of query 0 (multi-GPU shards)            */
   uint64_t seed;
   uint64_t offset;         /* RNG stream offset (one per engine call)               */
+  float* state;            /* optional particle state [n_slots + 1][B*S] (slot-major; the
+                              last row is the log-weight accumulator) for walks split into
+                              segments (resampled importance sampling)                 */
+  int32_t state_flags;     /* 1: load slots + log-weight from state before the first step;
+                              2: store them after the last step                        */
+  int32_t reserved_args;
 } vbn_walk_args;
 
 int vbn_hip_abi_version(void);
@@ -137,6 +146,15 @@ int vbn_hip_walk(const vbn_walk_args* args, void* stream);
  * log_w and w may alias. */
 int vbn_hip_normalize_weights(const float* log_w, float* w, float* ess, int64_t n_queries,
                               int32_t n_samples, int32_t normalize, float eps, void* stream);
+
+/* Multinomial resampling of a segmented walk's particle state (resampled_importance_sampling.py
+ * :33-41): per query b, S indices idx[s] ~ Categorical(w[b, :]) (inverse CDF of u[b][s] if u is
+ * given, else counter-based Philox keyed by (seed, offset, query q_base + b, s)), then
+ * state_out[c][b*S + s] = state_in[c][b*S + idx[s]] for the n_cols - 1 slot rows and
+ * state_out[n_cols - 1][.] = 0 (log-weights reset).  state_in and state_out must not alias. */
+int vbn_hip_resample(const float* w, const float* u, uint64_t seed, uint64_t offset, int64_t q_base,
+                     const float* state_in, float* state_out, int64_t n_queries, int32_t n_samples,
+                     int32_t n_cols, void* stream);
 
 /* Rao-Blackwellized target epilogue over P particles per query
  * (rao_blackwellized_marginalization.py:68-76, 255-317):

@@ -44,6 +44,10 @@ class TorchDraws:
     def randint(self, n: int, count: int) -> torch.Tensor:          # torch.randint(0, n, (k,))
         return torch.randint(0, n, (count,))
 
+    def multinomial(self, probs2d: torch.Tensor, n: int) -> torch.Tensor:
+        # resampled_importance_sampling.py:38
+        return torch.multinomial(probs2d, num_samples=n, replacement=True)
+
 
 class ReplayDraws:
     """Replays recorded draws in call order; checks kind and element count."""
@@ -76,6 +80,9 @@ class ReplayDraws:
 
     def randint(self, n: int, count: int) -> torch.Tensor:
         return self._next("randint", count)["index"].reshape(-1).clone()
+
+    def multinomial(self, probs2d: torch.Tensor, n: int) -> torch.Tensor:
+        return self._next("cat", probs2d.shape[0] * n)["index"].reshape(probs2d.shape[0], n).clone()
 
     def exhausted(self) -> bool:
         return self.pos == len(self.records)
@@ -763,3 +770,39 @@ def rao_blackwellized(model: BNModel, target: str, evidence: Dict, do: Dict, n_s
     z_norm = (x - mu) / sigma
     comp_pdf = torch.exp(-0.5 * z_norm ** 2) / (math.sqrt(2.0 * math.pi) * sigma)
     return (w.unsqueeze(-1) * comp_pdf).sum(dim=1), grid, None
+
+
+# ----------------------------------------------------------------------------------------
+# resampled_importance_sampling (reference vbn/inference/resampled_importance_sampling.py)
+# ----------------------------------------------------------------------------------------
+
+def resampled_importance_sampling(model: BNModel, target: str, evidence: Dict, do: Dict, n: int, draws,
+                                  ess_threshold: float = 0.5, resample: bool = True, clamp_obs: bool = True):
+    """resampled_importance_sampling.py:43-105; returns (weights, samples, last_ess, resampled)."""
+    b = _batch(evidence, do)
+    fixed = _fixed(evidence, do, clamp=clamp_obs)                                        # 56-58
+    cols, total = _layout(model)
+    samples = torch.zeros(b, n, total)
+    log_w = torch.zeros(b, n)
+    threshold = max(1.0, ess_threshold * float(n)) if ess_threshold <= 1.0 else float(ess_threshold)
+    last_ess, resampled = None, False
+    for node in model.topo:                                                              # 69-100
+        rec = model.cpds[node]
+        if node in fixed:
+            value = fixed[node].unsqueeze(1).expand(b, n, -1)
+            samples[..., cols[node]] = value
+            if node in evidence:
+                log_w = log_w + cpd_log_prob(rec, value, _gather_parents(model, node, samples, cols))
+                if resample:
+                    w = torch.softmax(log_w, dim=1)
+                    ess = 1.0 / (w ** 2).sum(dim=1)
+                    last_ess = ess
+                    if torch.any(ess < threshold):                                       # 33-41
+                        idx = draws.multinomial(torch.softmax(log_w, dim=1), n)
+                        samples = samples[torch.arange(b).unsqueeze(1), idx]
+                        log_w = torch.zeros_like(log_w)
+                        resampled = True
+            continue
+        samples[..., cols[node]] = cpd_sample(rec, _gather_parents(model, node, samples, cols), n, draws)
+    w = torch.softmax(log_w, dim=1)
+    return w, samples[..., cols[target]], last_ess, resampled

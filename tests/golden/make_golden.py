@@ -9,8 +9,8 @@ distribution exactly:
 * ``torch.randn_like`` / ``Normal.sample``  -> standard normal ``z`` (Normal.sample returns
   ``z*scale+loc``, bit-identical to ``torch.normal``);
 * ``torch.rand_like``                       -> uniform ``u``;
-* ``torch.multinomial(p, 1)``               -> inverse-CDF draw in fp64; the fixture stores
-  the chosen index AND the midpoint of its CDF interval (``u_mid``), so a consumer that
+* ``torch.multinomial(p, k)``               -> k inverse-CDF draws per row in fp64; the fixture
+  stores the chosen index AND the midpoint of its CDF interval (``u_mid``), so a consumer that
   recomputes the probabilities in fp32 picks the same index from ``u_mid``;
 * ``torch.randint(0, n, (k,))``             -> ``floor(u*n)``, stored as index and
   ``u_mid = (idx + 0.5) / n``.
@@ -85,7 +85,7 @@ class Recorder:
 
     def multinomial(self, probs, num_samples, replacement=False, *a, **k):
         if num_samples != 1:
-            raise RuntimeError("recorder supports num_samples == 1 only")
+            return self._multinomial_n(probs, int(num_samples), replacement)
         p = probs.detach().double()
         p = p / p.sum(-1, keepdim=True)
         cdf = p.cumsum(-1)
@@ -97,6 +97,22 @@ class Recorder:
                          torch.zeros_like(hi))
         self._rec("cat", 0.5 * (lo + hi), idx)
         return idx.unsqueeze(1)
+
+    def _multinomial_n(self, probs, n, replacement):
+        """multinomial(p, n, replacement=True) (resampled_importance_sampling.py:38): n inverse-
+        CDF draws per row, recorded as index + CDF-interval midpoint like the 1-draw case."""
+        if not replacement:
+            raise RuntimeError("recorder supports num_samples > 1 with replacement only")
+        p = probs.detach().double()
+        p = p / p.sum(-1, keepdim=True)
+        cdf = p.cumsum(-1)
+        cdf[:, -1] = 1.0
+        u = torch.rand(p.shape[0], n, generator=self.g, dtype=torch.float64)
+        idx = (cdf.unsqueeze(1) <= u.unsqueeze(-1)).sum(-1).clamp(max=p.shape[1] - 1)     # [b, n]
+        hi = cdf.gather(1, idx)
+        lo = torch.where(idx > 0, cdf.gather(1, (idx - 1).clamp(min=0)), torch.zeros_like(hi))
+        self._rec("cat", 0.5 * (lo + hi), idx)
+        return idx
 
     def normal_sample(self, dist, sample_shape=torch.Size()):
         shape = dist._extended_shape(torch.Size(sample_shape))

@@ -8,6 +8,9 @@ writes ``tests/golden/ext_*.pt``.  Cases:
   gaussian (linear_gaussian, gaussian_nn) and categorical (softmax_nn) targets, root targets,
   a fixed target, and both fallback reasons (observed descendant, unsupported target CPD);
   the fallback LW's draws are phase 1 (the unsupported-target case walks its particles first).
+* ``resampled_importance_sampling`` (resampled_importance_sampling.py:43-105): YAML defaults,
+  forced resampling, off-manifold evidence, resample off, absolute threshold, B = 1,
+  clamp_obs off; the resampling draws are engine-level (node None).
 
 Usage: python tests/golden/make_golden_ext.py [--out tests/golden]
 """
@@ -50,6 +53,29 @@ def run_rb(vbn, seed, query, n_samples, n_particles):
             out["outputs"] = {"pdf": pdf.clone(), "samples": samples.clone(),
                               "fallback": bool(eng._last_fallback),
                               "reason": str(eng._last_reason or "")}
+    finally:
+        G.untag_nodes(vbn)
+    out["draws"] = rec.records
+    return out
+
+
+def run_ris(vbn, seed, query, n_samples, **params):
+    rec = G.Recorder(seed)
+    out = {"engine": "resampled_importance_sampling", "params": dict(params), "n_samples": int(n_samples),
+           "query": {"target": query["target"],
+                     "evidence": {k: v.clone() for k, v in query.get("evidence", {}).items()},
+                     "do": {k: v.clone() for k, v in query.get("do", {}).items()}},
+           "seed": seed}
+    G.tag_nodes(vbn, rec)
+    try:
+        with rec:
+            vbn.set_inference_method("resampled_importance_sampling", n_samples=n_samples, **params)
+            pdf, samples = vbn.infer_posterior(query)
+            eng = vbn._inference
+            out["outputs"] = {"pdf": pdf.clone(), "samples": samples.clone(),
+                              "resampled": bool(eng._last_resampled)}
+            if eng._last_ess is not None:
+                out["outputs"]["ess"] = eng._last_ess.detach().clone()
     finally:
         G.untag_nodes(vbn)
     out["draws"] = rec.records
@@ -108,6 +134,33 @@ def main():
         cases.append(run_rb(vbn, s, q, 11, 24))
         s += 1
     fixtures["ext_rb_mix10"] = {"model": G.checkpoint_dict(vbn), "cases": cases}
+
+    # 3) resampled importance sampling on a 12-node five-family mix (kde included)
+    g12 = synthetic.random_dag(12, seed=11)
+    d12 = synthetic.sem_data(g12, 512, seed=0)
+    kinds = synthetic.round_robin_kinds(g12, ["gaussian_nn", "linear_gaussian", "mdn", "kde", "softmax_nn"])
+    extra = {nd: {"max_points": 48} for nd in g12.nodes if kinds[nd] == "kde"}
+    vbn = G.fit_model(vbn_mod, g12, kinds, d12, extra_kwargs=extra)
+    topo = list(nx.topological_sort(g12))
+    target = topo[-1]
+    ev_nodes = [x for x in topo[:-1]][1::3]
+    rows = torch.arange(3) * 11 + 4
+    ev = {a: d12[a][rows] for a in ev_nodes}
+    ev_off = {a: d12[a][rows] * 3.0 + 1.0 for a in ev_nodes}            # off-manifold: low ESS
+    q = {"target": target, "evidence": ev}
+    cases = [
+        run_ris(vbn, 201, q, 16),                                        # YAML defaults
+        run_ris(vbn, 202, q, 16, ess_threshold=20.0),                    # absolute > S: resample at every check
+        run_ris(vbn, 203, {"target": target, "evidence": ev_off}, 16),   # NaN ESS row never triggers
+        run_ris(vbn, 204, q, 16, resample=False),
+        run_ris(vbn, 205, q, 16, ess_threshold=15.97),                   # absolute threshold, some checks
+        run_ris(vbn, 206, {"target": target, "evidence": {k: v[:1] for k, v in ev.items()}}, 16,
+                ess_threshold=20.0),                                     # B = 1
+        run_ris(vbn, 207, q, 16, ess_threshold=20.0, clamp_obs=False),
+        run_ris(vbn, 208, {"target": ev_nodes[0], "evidence": {k: v for k, v in ev.items()
+                                                                 if k != ev_nodes[0]}}, 12, ess_threshold=0.9),
+    ]
+    fixtures["ext_ris_mix12"] = {"model": G.checkpoint_dict(vbn), "cases": cases}
 
     os.makedirs(args.out, exist_ok=True)
     for name, fx in fixtures.items():

@@ -18,7 +18,7 @@ def noise_dict(case: dict, model, phase: int = 0) -> Dict[str, Tuple[torch.Tenso
         S = int(case["params"]["n_particles"])        # the RB walk runs over the particles
     slots: Dict[str, Dict[int, list]] = {}
     for r in case["draws"]:
-        if r["phase"] != phase:
+        if r["phase"] != phase or r["node"] is None:       # node None: engine-level draws
             continue
         slot = 0 if r["kind"] in ("cat", "randint") else 1
         slots.setdefault(r["node"], {0: [], 1: []})[slot].append(r["value"].float())
@@ -35,3 +35,9 @@ def noise_dict(case: dict, model, phase: int = 0) -> Dict[str, Tuple[torch.Tenso
             s0 = v.view(v.numel() // (S * D), S, D) if per_dim0 else v.view(v.numel() // S, S)
         out[node] = (s0, s1)
     return out
+
+
+def resample_uniforms(case: dict):
+    """The engine-level multinomial resampling draws (node None), in order: list of [B, S]."""
+    S = int(case["n_samples"])
+    return [r["value"].float().view(-1, S) for r in case["draws"] if r["node"] is None and r["kind"] == "cat"]

@@ -15,7 +15,7 @@ import pytest
 import torch
 
 from conftest import golden_names, load_golden
-from golden_noise import noise_dict
+from golden_noise import noise_dict, resample_uniforms
 from oracle import vbn_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -115,6 +115,18 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
         xs = AncestralSampler(n_samples=n, kde_valu=kde_valu).sample(vbn, qq, n, _noise=nd0)
         rxs = O.ancestral(model, q["target"], q["evidence"], q["do"], n, draws)
         _close("samples", xs, rxs, S_ATOL, S_RTOL)
+    elif eng == "resampled_importance_sampling":
+        from vectorizedbayesiannetwork_amd.engines import ResampledImportanceSampling
+        e = ResampledImportanceSampling(n_samples=n, kde_valu=kde_valu, **p)
+        w, xs = e.infer_posterior(vbn, qq, _noise=nd0, _resample_u=[u.cuda() for u in resample_uniforms(case)])
+        rw, rxs, ress, rrs = O.resampled_importance_sampling(
+            model, q["target"], q["evidence"], q["do"], n, draws, ess_threshold=p.get("ess_threshold", 0.5),
+            resample=p.get("resample", True), clamp_obs=p.get("clamp_obs", True))
+        assert e._last_resampled == rrs == case["outputs"]["resampled"]
+        if ress is not None:
+            _close("ess", e._last_ess, ress, 1e-5, P_RTOL)
+        _close("samples", xs, rxs, S_ATOL, S_RTOL)
+        _close("weights", w, rw, P_ATOL, P_RTOL)
     elif eng == "rao_blackwellized_marginalization":
         from vectorizedbayesiannetwork_amd.engines import RaoBlackwellizedMarginalization
         e = RaoBlackwellizedMarginalization(n_samples=n, n_particles=p["n_particles"], kde_valu=kde_valu)

@@ -31,6 +31,13 @@ def _run_case(model, case):
         out = {"pdf": w, "samples": xs, "ess": ess, "fallback": fb}
     elif eng == "ancestral":
         out = {"samples": O.ancestral(model, q["target"], q["evidence"], q["do"], n, draws)}
+    elif eng == "resampled_importance_sampling":
+        w, xs, ess, rs = O.resampled_importance_sampling(
+            model, q["target"], q["evidence"], q["do"], n, draws, ess_threshold=p.get("ess_threshold", 0.5),
+            resample=p.get("resample", True), clamp_obs=p.get("clamp_obs", True))
+        out = {"pdf": w, "samples": xs, "resampled": rs}
+        if ess is not None:
+            out["ess"] = ess
     elif eng == "rao_blackwellized_marginalization":
         pdf, xs, reason = O.rao_blackwellized(model, q["target"], q["evidence"], q["do"], n,
                                               p["n_particles"], draws)

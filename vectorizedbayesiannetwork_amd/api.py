@@ -38,6 +38,8 @@ _ENGINE_DEFAULTS = {
         "likelihood_weighting": {"n_samples": 1024, "eps": 1e-12, "normalize": True},
         "rao_blackwellized_marginalization": {"n_samples": 256, "n_particles": 256, "stddevs": 4.0,
                                               "min_scale": 1e-6, "fallback": "likelihood_weighting"},
+        "resampled_importance_sampling": {"n_samples": 1024, "ess_threshold": 0.5, "resample": True,
+                                          "clamp_obs": True},
     },
     "sampling": {"ancestral": {"n_samples": 512}},
 }

@@ -1270,6 +1270,11 @@ __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) 
   L.s = (int)(L.p - L.b * A.n_samples);
 
   float lp = 0.f;
+  if (A.state && (A.state_flags & 1)) {             // resume a segmented walk
+    for (int c = 0; c < A.n_slots; ++c) vwrite(L, c, A.state[(int64_t)c * total + L.p]);
+    lp = A.state[(int64_t)A.n_slots * total + L.p];
+    wave_sync();
+  }
   for (int i = 0; i < A.n_steps; ++i) {
     const vbn_step st = steps[i];
     if (st.role == VBN_ROLE_SKIP) continue;
@@ -1288,6 +1293,10 @@ __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) 
     wave_sync();
   }
   if (!valid) return;
+  if (A.state && (A.state_flags & 2)) {
+    for (int c = 0; c < A.n_slots; ++c) A.state[(int64_t)c * total + L.p] = vread(L, c);
+    A.state[(int64_t)A.n_slots * total + L.p] = lp;
+  }
   if (A.out_lp && A.mode != VBN_MODE_SAMPLE) A.out_lp[L.p] = (A.mode == VBN_MODE_MCM) ? __expf(lp) : lp;
   if (A.out_x) {
     for (int k = 0; k < A.n_out_cols; ++k)
@@ -1364,6 +1373,58 @@ __global__ void __launch_bounds__(NW_THREADS) vbn_normalize_kernel(const float* 
     float t = 0.f;
     for (int k = 0; k < NW_THREADS / WAVE; ++k) t += red[k];
     if (ess) ess[row] = 1.0f / t;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// multinomial resampling (resampled_importance_sampling.py:33-41): one 256-thread workgroup per
+// query; inclusive CDF of the weights in LDS, one binary search per draw, state rows gathered
+// slot-major (coalesced writes, reads within the query's row of particles).
+// ------------------------------------------------------------------------------------------
+#define RS_THREADS 256
+
+__global__ void __launch_bounds__(RS_THREADS) vbn_resample_kernel(
+    const float* __restrict__ w, const float* __restrict__ u, uint64_t seed, uint64_t offset, int64_t q_base,
+    const float* __restrict__ sin, float* __restrict__ sout, int S, int n_cols, int64_t total) {
+  extern __shared__ __attribute__((aligned(16))) float cdf[];
+  __shared__ float seg[RS_THREADS];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* wr = w + b * S;
+  // inclusive prefix sum: each thread a contiguous segment, then the segment totals
+  const int per = (S + RS_THREADS - 1) / RS_THREADS;
+  const int s0 = min(S, tid * per), s1 = min(S, s0 + per);
+  float acc = 0.f;
+  for (int s = s0; s < s1; ++s) { acc += wr[s]; cdf[s] = acc; }
+  seg[tid] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    float run = 0.f;
+    for (int k = 0; k < RS_THREADS; ++k) { const float v = seg[k]; seg[k] = run; run += v; }
+  }
+  __syncthreads();
+  const float base = seg[tid];
+  for (int s = s0; s < s1; ++s) cdf[s] += base;
+  __syncthreads();
+  const float tot = cdf[S - 1];
+  for (int s = tid; s < S; s += RS_THREADS) {
+    float uu;
+    if (u) {
+      uu = u[b * S + s];
+    } else {
+      const uint2 r = philox2x32(make_uint2((uint32_t)s, (uint32_t)(q_base + b + 1) ^ (uint32_t)(seed >> 32)),
+                                 (uint32_t)seed + 0x7f000000u + (uint32_t)(offset & 0xffffffu));
+      uu = u01(r.x);
+    }
+    const float thr = uu * tot;
+    int lo = 0, hi = S - 1;                       // first k with cdf[k] > thr
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cdf[mid] > thr) hi = mid; else lo = mid + 1;
+    }
+    const int64_t src = b * S + lo, dst = b * S + s;
+    for (int c = 0; c + 1 < n_cols; ++c) sout[(int64_t)c * total + dst] = sin[(int64_t)c * total + src];
+    sout[(int64_t)(n_cols - 1) * total + dst] = 0.f;
   }
 }
 
@@ -1493,7 +1554,8 @@ extern "C" int64_t vbn_hip_lds_bytes(int32_t n_slots, int32_t max_out) {
 }
 
 extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
-  if (!a || !a->steps || !a->params || a->n_samples <= 0 || a->n_queries <= 0 || a->n_slots <= 0)
+  if (!a || (!a->steps && a->n_steps > 0) || a->n_steps < 0 || !a->params || a->n_samples <= 0 ||
+      a->n_queries <= 0 || a->n_slots <= 0)
     return fail(VBN_E_ARGS, "vbn_hip_walk: bad arguments");
   if (a->out_x && (!a->out_cols || a->n_out_cols <= 0))
     return fail(VBN_E_ARGS, "vbn_hip_walk: out_x without out_cols");
@@ -1523,6 +1585,21 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
     case 31u: hipLaunchKernelGGL(vbn_walk_kernel<31u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
     default: hipLaunchKernelGGL(vbn_walk_kernel<63u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
   }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  return 0;
+}
+
+extern "C" int vbn_hip_resample(const float* w, const float* u, uint64_t seed, uint64_t offset, int64_t q_base,
+                                const float* state_in, float* state_out, int64_t n_queries, int32_t n_samples,
+                                int32_t n_cols, void* stream) {
+  if (!w || !state_in || !state_out || state_in == state_out || n_queries <= 0 || n_samples <= 0 || n_cols <= 0)
+    return fail(VBN_E_ARGS, "vbn_hip_resample: bad arguments");
+  const size_t lds = (size_t)n_samples * sizeof(float);
+  if (lds > 64 * 1024) return fail(VBN_E_LDS, "vbn_hip_resample: more than 16384 samples per query");
+  hipLaunchKernelGGL(vbn_resample_kernel, dim3((unsigned)n_queries), dim3(RS_THREADS), lds, (hipStream_t)stream,
+                     w, u, seed, offset, q_base, state_in, state_out, n_samples, n_cols,
+                     n_queries * (int64_t)n_samples);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;

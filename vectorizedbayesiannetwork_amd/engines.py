@@ -21,6 +21,10 @@ Semantics mirror the reference branch by branch:
   non-descendants with the target written as its conditional parameters, then one epilogue
   launch (weights, mixture moments, grid density / categorical marginal); fallback engine for
   observed descendants and unsupported target CPDs.
+* RIS (resampled_importance_sampling.py:43-105): the LW walk split after every evidence node;
+  between segments the particle state stays in HBM, per-query softmax + ESS, and when any
+  query's ESS is below the threshold (batch-global, host sync as the reference) one
+  multinomial resampling launch for the whole batch.
 
 RNG: counter-based Philox keyed by ``(seed, offset, node, query, sample)``.  The seed of a
 call is taken from the global torch generator (so ``torch.manual_seed`` makes runs
@@ -47,6 +51,7 @@ __all__ = [
     "LikelihoodWeighting",
     "AncestralSampler",
     "RaoBlackwellizedMarginalization",
+    "ResampledImportanceSampling",
     "infer_batch_size",
 ]
 
@@ -183,8 +188,10 @@ def noise_tensor(pk: PackedModel, plan: QueryPlan, noise: Dict[str, Tuple], b: i
 
 def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: int, *,
              seed: int, offset: int = 0, q_base: int = 0, noise=None,
-             fixed_per_particle: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
-    """One launch of the particle walk; returns (lp [b,n] or empty, x [b,n,n_out_cols])."""
+             fixed_per_particle: bool = False, state: Optional[torch.Tensor] = None, state_flags: int = 0,
+             step_begin: int = 0, step_end: int = -1) -> Tuple[torch.Tensor, torch.Tensor]:
+    """One launch of the particle walk; returns (lp [b,n] or empty, x [b,n,n_out_cols]).
+    ``state``/``state_flags``/``step_begin``/``step_end``: one segment of a split walk."""
     n_out_cols = int(plan.out_cols.numel()) if plan.out_nodes else 0
     noise_b = 1
     if isinstance(noise, dict):
@@ -197,10 +204,14 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
         if noise.shape[3] != n or noise.shape[4] != pk.dmax:
             raise ValueError(f"noise must be [n_latent, 2, B|1, {n}, {pk.dmax}]")
     LAST_LAUNCH.update(pk=pk, plan=plan, fixed=fixed, b=b, n=n, fixed_per_particle=fixed_per_particle)
-    lp, x = ops.walk(plan.steps, plan.in_cols, pk.params, fixed, noise, plan.out_cols, b, n,
-                     plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
-                     len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
-                     plan.mode != MODE_SAMPLE, plan.kind_mask)
+    args = (plan.steps, plan.in_cols, pk.params, fixed, noise, plan.out_cols, b, n,
+            plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
+            len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
+            plan.mode != MODE_SAMPLE, plan.kind_mask)
+    if state is None:
+        lp, x = ops.walk(*args)
+    else:
+        lp, x = ops.walk_segment(*args, state, state_flags, step_begin, step_end)
     if plan.mode != MODE_SAMPLE:
         lp = lp.view(b, n)
     if n_out_cols:
@@ -450,6 +461,73 @@ class RaoBlackwellizedMarginalization(_EngineBase):
         pdf, _ = ops.rb_epilogue(log_w, prm, log_w.new_empty(0), c, 1, self.stddevs, self.min_scale, 1e-12)
         support = rec.state["_sample_values"][0].to(device=dev, dtype=torch.float32)
         return pdf, support.view(1, -1, 1).expand(b, -1, 1)
+
+
+@register_inference("resampled_importance_sampling")
+class ResampledImportanceSampling(_EngineBase):
+    """resampled_importance_sampling.py:13-105 on the GPU (segmented walk + resampling)."""
+
+    def __init__(self, n_samples: int = 512, ess_threshold: float = 0.5, resample: bool = True,
+                 clamp_obs: bool = True, **kwargs):
+        super().__init__(n_samples=n_samples, **kwargs)
+        self.ess_threshold = float(ess_threshold)
+        self.resample = bool(resample)
+        self.clamp_obs = bool(clamp_obs)
+        self._last_ess: Optional[torch.Tensor] = None
+        self._last_resampled = False
+
+    def infer_posterior(self, vbn, query, **kwargs):
+        n = int(kwargs.get("n_samples", self.n_samples))
+        thr_in = float(kwargs.get("ess_threshold", self.ess_threshold))
+        resample = bool(kwargs.get("resample", self.resample))
+        clamp = bool(kwargs.get("clamp_obs", self.clamp_obs))
+        target, ev, do = self._query(query)
+        b = infer_batch_size(ev, do)
+        dev = _device_of(vbn)
+        pk = packed_model(vbn, dev)
+        model = pk.model
+        vals = _fixed_values(query, dev, clamp=clamp)
+        _check_discrete(pk, vals, list(ev))
+        key = ("ris", target, tuple(sorted(ev)), tuple(sorted(do)), clamp)
+        plan = self._plan(pk, key, latent=[x for x in model.topo if x not in vals],
+                          fixed=[x for x in model.topo if x in vals], logp=[x for x in model.topo if x in ev],
+                          out_nodes=[target], shared_roots=True, mode=MODE_WEIGHTED)
+        fx = _fixed_buffer(plan, vals, b, dev)
+        seed = self._seed(kwargs)
+        noise = kwargs.get("_noise")
+        if isinstance(noise, dict):
+            noise = noise_tensor(pk, plan, noise, b, n)
+        u_list = list(kwargs.get("_resample_u") or [])
+        threshold = max(1.0, thr_in * float(n)) if thr_in <= 1.0 else thr_in            # 62-65
+        self._last_resampled = False
+        order = [x for x in model.topo]                                                 # plan order
+        cuts = [i + 1 for i, x in enumerate(order) if x in ev] if resample else []      # 75-90
+        cuts = [c for c in cuts if c < len(order)] + [len(order)]
+        if len(cuts) == 1:
+            log_w, xs = run_walk(pk, plan, fx, b, n, seed=seed, q_base=self.q_base, noise=noise)
+        else:
+            total = b * n
+            st_a = torch.empty(plan.n_slots + 1, total, device=dev, dtype=torch.float32)
+            st_b = torch.empty_like(st_a)
+            begin, events = 0, 0
+            for k, end in enumerate(cuts):
+                last = k == len(cuts) - 1
+                flags = (1 if k > 0 else 0) | (0 if last else 2)
+                log_w, xs = run_walk(pk, plan, fx, b, n, seed=seed, q_base=self.q_base, noise=noise,
+                                     state=st_a, state_flags=flags, step_begin=begin, step_end=end)
+                begin = end
+                if last:
+                    break
+                w, ess = ops.normalize_weights(st_a[plan.n_slots].view(b, n), True, 0.0)     # 85-87
+                self._last_ess = ess
+                if bool((ess < threshold).any()):                                            # 88-90
+                    u = u_list.pop(0) if u_list else None
+                    ops.resample(w, u, seed, events + 1, self.q_base, st_a, st_b)
+                    st_a, st_b = st_b, st_a
+                    events += 1
+                    self._last_resampled = True
+        w, _ = ops.normalize_weights(log_w, True, 0.0)                                     # 102
+        return w, xs
 
 
 @register_sampling("ancestral")

@@ -1,8 +1,10 @@
 """PyTorch-ROCm custom ops over the C-ABI (``torch.ops.vbn_hip.*``).
 
 * ``vbn_hip::walk``               -> ``vbn_hip_walk``             (particle pass)
+* ``vbn_hip::walk_segment``       -> ``vbn_hip_walk``             (one segment of a split pass)
 * ``vbn_hip::normalize_weights``  -> ``vbn_hip_normalize_weights`` (softmax over S + ESS)
 * ``vbn_hip::rb_epilogue``        -> ``vbn_hip_rb_epilogue``       (Rao-Blackwellized target)
+* ``vbn_hip::resample``           -> ``vbn_hip_resample``          (multinomial particle resampling)
 
 Both run asynchronously on the current HIP stream, allocate fresh contiguous outputs and
 have fake (meta) implementations for shape inference.  Host-side checks make sure every
@@ -19,7 +21,7 @@ from torch import Tensor
 from . import _lib
 from .plan import STEP_INTS
 
-__all__ = ["walk", "normalize_weights", "rb_epilogue"]
+__all__ = ["walk", "walk_segment", "normalize_weights", "rb_epilogue", "resample"]
 
 
 def _ptr(t: Optional[Tensor]) -> Optional[int]:
@@ -42,6 +44,37 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
          fixed_ld: int, fixed_per_particle: bool, noise_b: int, n_noise: int, dmax: int,
          n_out_cols: int, mode: int, q_base: int, seed: int, offset: int,
          want_lp: bool, kind_mask: int = 63) -> Tuple[Tensor, Tensor]:
+    """One particle walk over the whole step table."""
+    return _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots,
+                        max_out, fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode,
+                        q_base, seed, offset, want_lp, kind_mask, None, 0, 0, -1)
+
+
+@torch.library.custom_op("vbn_hip::walk_segment", mutates_args=("state",))
+def walk_segment(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: Optional[Tensor],
+                 out_cols: Tensor, n_queries: int, n_samples: int, n_slots: int, max_out: int,
+                 fixed_ld: int, fixed_per_particle: bool, noise_b: int, n_noise: int, dmax: int,
+                 n_out_cols: int, mode: int, q_base: int, seed: int, offset: int,
+                 want_lp: bool, kind_mask: int, state: Tensor, state_flags: int, step_begin: int,
+                 step_end: int) -> Tuple[Tensor, Tensor]:
+    """One segment steps[step_begin:step_end] of a split walk; ``state`` [n_slots + 1, B*S]
+    carries node values and log-weights between segments (state_flags 1 = load, 2 = store)."""
+    return _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots,
+                        max_out, fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode,
+                        q_base, seed, offset, want_lp, kind_mask, state, state_flags, step_begin, step_end)
+
+
+@walk_segment.register_fake
+def _walk_segment_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
+                       fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
+                       offset, want_lp, kind_mask, state, state_flags, step_begin, step_end):
+    total = n_queries * n_samples
+    return params.new_empty(total if want_lp else 0), params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))
+
+
+def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
+                 fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
+                 offset, want_lp, kind_mask, state, state_flags, step_begin, step_end):
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::walk runs on the GPU only (no CPU fallback); "
@@ -53,7 +86,16 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
     _check_dev("fixed", fixed, torch.float32, device)
     if steps.dim() != 2 or steps.shape[1] != STEP_INTS:
         raise ValueError("vbn_hip::walk: steps must be [n_steps, 32]")
+    step_end = steps.shape[0] if step_end < 0 else step_end
+    if not 0 <= step_begin <= step_end <= steps.shape[0]:
+        raise ValueError(f"vbn_hip::walk: bad step range [{step_begin}, {step_end})")
     total = n_queries * n_samples
+    if state_flags:
+        if state is None:
+            raise ValueError("vbn_hip::walk: state_flags without a state buffer")
+        _check_dev("state", state, torch.float32, device)
+        if state.numel() < (n_slots + 1) * total:
+            raise ValueError(f"vbn_hip::walk: state has {state.numel()} values, needs {(n_slots + 1) * total}")
     rows = total if fixed_per_particle else n_queries
     if fixed.numel() < rows * fixed_ld:
         raise ValueError(f"vbn_hip::walk: fixed buffer has {fixed.numel()} values, needs {rows}x{fixed_ld}")
@@ -65,7 +107,7 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
     lp = torch.empty(total if want_lp else 0, device=device, dtype=torch.float32)
     x = torch.empty((total, n_out_cols) if n_out_cols > 0 else (0,), device=device, dtype=torch.float32)
     a = _lib.VbnWalkArgs()
-    a.steps = _ptr(steps)
+    a.steps = steps.data_ptr() + step_begin * STEP_INTS * 4 if step_end > step_begin else None
     a.in_cols = _ptr(in_cols)
     a.params = _ptr(params)
     a.fixed = _ptr(fixed)
@@ -75,7 +117,9 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
     a.out_x = _ptr(x)
     a.n_queries = n_queries
     a.n_samples = n_samples
-    a.n_steps = steps.shape[0]
+    a.n_steps = step_end - step_begin
+    a.state = _ptr(state) if state_flags else None
+    a.state_flags = int(state_flags)
     a.n_slots = n_slots
     a.max_out = max_out
     a.fixed_ld = fixed_ld
@@ -157,3 +201,35 @@ def rb_epilogue(log_w: Tensor, params: Tensor, z: Tensor, n_out: int, mode: int,
 def _rb_fake(log_w, params, z, n_out, mode, stddevs, min_scale, eps):
     b = log_w.shape[0]
     return log_w.new_empty(b, n_out), log_w.new_empty((b, n_out) if mode == 0 else (0,))
+
+
+@torch.library.custom_op("vbn_hip::resample", mutates_args=("state_out",))
+def resample(w: Tensor, u: Optional[Tensor], seed: int, offset: int, q_base: int, state_in: Tensor,
+             state_out: Tensor) -> None:
+    """w [B,S] normalized weights; state_in/state_out [n_cols, B*S] (last row: log-weights,
+    reset to 0); u [B,S] injected uniforms or None (Philox)."""
+    if w.device.type != "cuda" or w.dtype != torch.float32 or w.dim() != 2:
+        raise ValueError("vbn_hip::resample: w must be a float32 [B,S] GPU tensor")
+    b, s = w.shape
+    for name, t in (("state_in", state_in), ("state_out", state_out)):
+        _check_dev(name, t, torch.float32, w.device)
+        if t.dim() != 2 or t.shape[1] != b * s:
+            raise ValueError(f"vbn_hip::resample: {name} must be [n_cols, {b * s}]")
+    if state_in.shape != state_out.shape or state_in.data_ptr() == state_out.data_ptr():
+        raise ValueError("vbn_hip::resample: state_in and state_out must be distinct buffers of one shape")
+    w = w.contiguous()
+    if u is not None:
+        u = u.to(device=w.device, dtype=torch.float32).contiguous()
+        if u.numel() != b * s:
+            raise ValueError("vbn_hip::resample: u must be [B,S]")
+    lib = _lib.load()
+    with torch.cuda.device(w.device):
+        _lib.check(lib.vbn_hip_resample(
+            _ptr(w), _ptr(u), seed & ((1 << 64) - 1), offset & ((1 << 64) - 1), q_base, _ptr(state_in),
+            _ptr(state_out), b, s, state_in.shape[0], ctypes.c_void_p(_stream_handle(w.device))),
+            "vbn_hip_resample")
+
+
+@resample.register_fake
+def _resample_fake(w, u, seed, offset, q_base, state_in, state_out):
+    return None

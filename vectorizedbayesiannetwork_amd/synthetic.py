@@ -81,6 +81,8 @@ CONFIGS = {
     # §8(f) row on the cfg2 DAG: Rao-Blackwellized target (P = S = 1024)
     "rb32": dict(name="32node-gaussian_nn-rb", n_nodes=32, kinds=("gaussian_nn",),
                  engine="rao_blackwellized_marginalization", B=4096, S=1024, rows=2048),
+    "ris32": dict(name="32node-gaussian_nn-ris", n_nodes=32, kinds=("gaussian_nn",),
+                  engine="resampled_importance_sampling", B=4096, S=1024, rows=2048),
     "anchor64": dict(name="64node-gaussian_nn-mcm", n_nodes=64, kinds=("gaussian_nn",),
                      engine="monte_carlo_marginalization", B=4096, S=1024, rows=2048),
 }
