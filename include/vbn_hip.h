@@ -23,6 +23,8 @@
  *                             MDNCPD          (vbn/cpds/mdn.py:185-272)
  *                             KDECPD          (vbn/cpds/kde.py:105-182)
  *                             SoftmaxNNCPD    (vbn/cpds/softmax_nn.py:581-759).
+ *   vbn_hip_posterior_stats VBN._posterior_stats (vbn/vbn.py:483-504), the summary behind
+ *                             VBN.infer_relative (vbn/vbn.py:519-568)
  *   vbn_hip_resample        the multinomial resampling step of
  *                             ResampledImportanceSampling._resample
  *                               (vbn/inference/resampled_importance_sampling.py:33-41)
@@ -155,6 +157,13 @@ int vbn_hip_normalize_weights(const float* log_w, float* w, float* ess, int64_t 
 int vbn_hip_resample(const float* w, const float* u, uint64_t seed, uint64_t offset, int64_t q_base,
                      const float* state_in, float* state_out, int64_t n_queries, int32_t n_samples,
                      int32_t n_cols, void* stream);
+
+/* Weighted posterior summary per query (vbn.py:483-504, _posterior_stats):
+ *   w = nan/inf -> 0, clamp >= 0, normalised (uniform 1/S where the sum <= eps);
+ *   mean[b][d] = sum_s w x[b][s][d]; std[b][d] = sqrt(max(sum_s w (x - mean)^2, 0));
+ *   ess[b] = 1 / max(sum_s w^2, eps).   pdf [B][S], x [B][S][D] contiguous. */
+int vbn_hip_posterior_stats(const float* pdf, const float* x, float* mean, float* std, float* ess,
+                            int64_t n_queries, int32_t n_samples, int32_t dim, float eps, void* stream);
 
 /* Rao-Blackwellized target epilogue over P particles per query
  * (rao_blackwellized_marginalization.py:68-76, 255-317):

@@ -806,3 +806,20 @@ def resampled_importance_sampling(model: BNModel, target: str, evidence: Dict, d
         samples[..., cols[node]] = cpd_sample(rec, _gather_parents(model, node, samples, cols), n, draws)
     w = torch.softmax(log_w, dim=1)
     return w, samples[..., cols[target]], last_ess, resampled
+
+
+# ----------------------------------------------------------------------------------------
+# posterior summary (reference vbn/vbn.py:483-504)
+# ----------------------------------------------------------------------------------------
+
+def posterior_stats(pdf: torch.Tensor, samples: torch.Tensor, eps: float = 1e-12) -> Dict[str, torch.Tensor]:
+    """VBN._posterior_stats (vbn.py:495-504)."""
+    weights = torch.nan_to_num(pdf, nan=0.0, posinf=0.0, neginf=0.0).clamp_min(0.0)
+    denom = weights.sum(dim=1, keepdim=True)
+    uniform = torch.full_like(weights, 1.0 / max(1, weights.shape[1]))
+    weights = torch.where(denom > eps, weights / denom.clamp_min(eps), uniform)
+    mean = (weights.unsqueeze(-1) * samples).sum(dim=1)
+    var = (weights.unsqueeze(-1) * (samples - mean.unsqueeze(1)) ** 2).sum(dim=1)
+    std = var.clamp_min(0.0).sqrt()
+    ess = 1.0 / (weights ** 2).sum(dim=1).clamp_min(eps)
+    return {"mean": mean, "std": std, "ess": ess}

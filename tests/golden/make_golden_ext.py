@@ -11,6 +11,8 @@ writes ``tests/golden/ext_*.pt``.  Cases:
 * ``resampled_importance_sampling`` (resampled_importance_sampling.py:43-105): YAML defaults,
   forced resampling, off-manifold evidence, resample off, absolute threshold, B = 1,
   clamp_obs off; the resampling draws are engine-level (node None).
+* ``posterior_stats`` (VBN._posterior_stats, vbn.py:483-504) on engine outputs and on
+  edge-case weights (zero mass, NaN, +-inf, negative).
 
 Usage: python tests/golden/make_golden_ext.py [--out tests/golden]
 """
@@ -159,8 +161,36 @@ def main():
         run_ris(vbn, 207, q, 16, ess_threshold=20.0, clamp_obs=False),
         run_ris(vbn, 208, {"target": ev_nodes[0], "evidence": {k: v for k, v in ev.items()
                                                                  if k != ev_nodes[0]}}, 12, ess_threshold=0.9),
+        # the last node is evidence: the ESS check (and resampling) after the final node
+        run_ris(vbn, 209, {"target": ev_nodes[0], "evidence": {**{k: v for k, v in ev.items() if k != ev_nodes[0]},
+                                                              target: d12[target][rows]}}, 12, ess_threshold=20.0),
     ]
     fixtures["ext_ris_mix12"] = {"model": G.checkpoint_dict(vbn), "cases": cases}
+
+    # 4) posterior summaries (vbn.py:483-504) of engine outputs and edge-case weights
+    gen = torch.Generator().manual_seed(3)
+    inputs = []
+    for fx in fixtures.values():
+        for c in fx["cases"][:4]:
+            o = c["outputs"]
+            if o["pdf"].dim() == 2 and o["samples"].dim() == 3 and o["pdf"].shape[:2] == o["samples"].shape[:2]:
+                inputs.append((o["pdf"].clone(), o["samples"].clone()))
+    w = torch.rand(4, 32, generator=gen)
+    x = torch.randn(4, 32, 2, generator=gen)
+    w_edge = w.clone()
+    w_edge[0] = 0.0                                   # zero mass -> uniform weights
+    w_edge[1, :5] = float("nan")
+    w_edge[2, 3] = float("inf")
+    w_edge[2, 4] = -float("inf")
+    w_edge[3, :10] = -1.0                             # negative entries clamp to 0
+    inputs += [(w, x), (w_edge, x)]
+    scases = []
+    for pdf, xs in inputs:
+        st = vbn._posterior_stats(pdf, xs)
+        scases.append({"engine": "posterior_stats", "params": {}, "n_samples": int(pdf.shape[1]),
+                       "pdf": pdf, "samples_in": xs, "draws": [],
+                       "outputs": {k: v.clone() for k, v in st.items()}})
+    fixtures["ext_stats"] = {"model": G.checkpoint_dict(vbn), "cases": scases}
 
     os.makedirs(args.out, exist_ok=True)
     for name, fx in fixtures.items():

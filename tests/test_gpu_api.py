@@ -1,0 +1,59 @@
+"""Facade-level behaviour on the GPU that the golden cases do not cover directly
+(reference tests/test_gaussian_exact_relative.py:40-57, tests/test_rao_blackwellized_marginalization.py)."""
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _chain_vbn():
+    from vectorizedbayesiannetwork_amd import VBN
+    from vectorizedbayesiannetwork_amd.model import model_from_checkpoint
+    return VBN.from_model(model_from_checkpoint(load_golden("ext_rb_chain")["model"]), device="cuda")
+
+
+def test_infer_relative_shapes_and_direction():
+    """x -> y linear chain (y ~ 1.2 x + 0.3): shifting the evidence up moves the posterior mean up."""
+    vbn = _chain_vbn()
+    vbn.set_inference_method("likelihood_weighting", n_samples=2048)
+    torch.manual_seed(0)
+    out = vbn.infer_relative(query={"target": "y", "evidence": {"x": torch.tensor([[1.0], [1.5]])}},
+                             reference_query={"target": "y", "evidence": {"x": torch.tensor([[0.0]])}})
+    assert out["target"] == "y"
+    for k in ("delta_mean", "delta_std", "relative_mean_change", "relative_std_change"):
+        assert out[k].shape == (2, 1) and torch.isfinite(out[k]).all()
+    assert (out["delta_mean"] > 0).all()
+    assert out["query_stats"]["effective_sample_size"].shape == (2,)
+    with pytest.raises(ValueError, match="same target"):
+        vbn.infer_relative({"target": "y", "evidence": {"x": torch.zeros(1, 1)}}, {"target": "z"})
+
+
+def test_rb_mean_tracks_linear_conditional():
+    """reference test_rb_marginalizes_missing_parents_for_linear_gaussian, on the GPU engine."""
+    vbn = _chain_vbn()
+    vbn.set_inference_method("rao_blackwellized_marginalization", n_samples=81, n_particles=256)
+    pdf, samples = vbn.infer_posterior({"target": "y", "evidence": {"x": torch.tensor([[0.4]])}})
+    assert pdf.shape == (1, 81) and samples.shape == (1, 81, 1)
+    assert torch.isfinite(pdf).all() and torch.isfinite(samples).all()
+    assert vbn._inference._last_fallback is False
+    w = pdf / pdf.sum(dim=1, keepdim=True).clamp_min(1e-12)
+    mean = (w.unsqueeze(-1) * samples).sum(dim=1).squeeze()
+    rec = vbn.model.cpds["y"]
+    expected = (torch.tensor([0.4]) @ rec.state["_weight"] + rec.state["_bias"]).squeeze()
+    assert torch.allclose(mean.cpu(), expected, atol=0.25, rtol=0.15)
+    vbn.set_inference_method("rao_blackwellized_marginalization", n_samples=9, n_particles=128)
+    pdf, samples = vbn.infer_posterior({"target": "y", "evidence": {"z": torch.tensor([[0.2]])}})
+    assert pdf.shape == (1, 9) and vbn._inference._last_fallback is True
+
+
+def test_ris_production_rng_runs_and_normalizes():
+    """RIS with Philox draws (no injected noise): weights normalised per query, resampling
+    triggered by a threshold above S."""
+    vbn = _chain_vbn()
+    vbn.set_inference_method("resampled_importance_sampling", n_samples=512, ess_threshold=600.0)
+    w, xs = vbn.infer_posterior({"target": "y", "evidence": {"z": torch.tensor([[0.2], [-0.4]])}})
+    assert w.shape == (2, 512) and xs.shape == (2, 512, 1)
+    assert torch.allclose(w.sum(dim=1).cpu(), torch.ones(2), atol=1e-5)
+    assert vbn._inference._last_resampled is True

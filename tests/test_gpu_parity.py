@@ -55,7 +55,7 @@ def _cases():
         has_kde = any(str(v["cpd_key"]) == "kde" for v in fx["model"]["nodes"].values())
         for i, case in enumerate(fx["cases"]):
             out.append(pytest.param(name, i, False, id=f"{name}-{i}-{case['engine']}"))
-            if has_kde and case["engine"] != "cpd":
+            if has_kde and case["engine"] not in ("cpd", "posterior_stats"):
                 # the alternative KDE distance path (packed VALU)
                 out.append(pytest.param(name, i, True, id=f"{name}-{i}-{case['engine']}-kde_valu"))
     return out
@@ -84,6 +84,12 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
         if "x" in case:
             lpx = C.cpd_log_prob(vbn, node, case["x"].cuda(), None if par is None else par.cuda())
             _close("cpd.log_prob(x)", lpx, O.cpd_log_prob(rec, case["x"], par), 2e-4, 1e-4)
+        return
+    if eng == "posterior_stats":
+        st = vbn._posterior_stats(case["pdf"].cuda(), case["samples_in"].cuda())
+        ref = O.posterior_stats(case["pdf"], case["samples_in"])
+        for k in ("mean", "std", "ess"):
+            _close(k, st[k], ref[k], 1e-5, 1e-4)
         return
     q = case["query"]
     qq = vbn._normalize_query(q)

@@ -13,6 +13,8 @@ from vectorizedbayesiannetwork_amd.model import model_from_checkpoint
 
 
 def _run_case(model, case):
+    if case["engine"] == "posterior_stats":
+        return O.posterior_stats(case["pdf"], case["samples_in"])
     q = case["query"]
     n = case["n_samples"]
     draws = O.ReplayDraws(case["draws"])

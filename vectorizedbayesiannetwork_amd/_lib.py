@@ -22,6 +22,7 @@ EXPORTS = (
     "vbn_hip_normalize_weights",
     "vbn_hip_rb_epilogue",
     "vbn_hip_resample",
+    "vbn_hip_posterior_stats",
     "vbn_hip_lds_bytes",
     "vbn_hip_struct_size",
 )
@@ -103,6 +104,10 @@ def load(path: str = None) -> ctypes.CDLL:
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int64,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
         lib.vbn_hip_resample.restype = ctypes.c_int
+        lib.vbn_hip_posterior_stats.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
+        lib.vbn_hip_posterior_stats.restype = ctypes.c_int
         lib.vbn_hip_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
         lib.vbn_hip_lds_bytes.restype = ctypes.c_int64
         lib.vbn_hip_struct_size.argtypes = [ctypes.c_int]

@@ -212,6 +212,59 @@ class VBN:
             return {k: v.detach() for k, v in out.items()}
         return out.detach()
 
+    # ---- posterior summaries (vbn.py:483-568) ---------------------------------------------
+    def _posterior_stats(self, pdf: torch.Tensor, samples: torch.Tensor, *, eps: float = 1e-12
+                         ) -> Dict[str, torch.Tensor]:
+        """reference vbn.py:483-504, one HIP launch (vbn_hip_posterior_stats)."""
+        from . import ops
+        if pdf.dim() != 2:
+            raise ValueError(f"Expected pdf with shape [B,S], got {tuple(pdf.shape)}")
+        if samples.dim() != 3:
+            raise ValueError(f"Expected samples with shape [B,S,D], got {tuple(samples.shape)}")
+        if pdf.shape[0] != samples.shape[0] or pdf.shape[1] != samples.shape[1]:
+            raise ValueError("pdf and samples shapes are incompatible.")
+        mean, std, ess = ops.posterior_stats(pdf, samples, float(eps))
+        return {"mean": mean, "std": std, "ess": ess}
+
+    @staticmethod
+    def _broadcast_batch(a: torch.Tensor, b: torch.Tensor):
+        """reference vbn.py:506-517"""
+        if a.shape[0] == b.shape[0]:
+            return a, b
+        if a.shape[0] == 1:
+            return a.expand(b.shape[0], *a.shape[1:]), b
+        if b.shape[0] == 1:
+            return a, b.expand(a.shape[0], *b.shape[1:])
+        raise ValueError("Query and reference batch sizes must match, unless one of them is 1.")
+
+    def infer_relative(self, query, reference_query=None, *, eps: float = 1e-12, **kwargs):
+        """reference vbn.py:519-568: posterior of ``query`` relative to ``reference_query``
+        (default: the same target without evidence)."""
+        q = self._normalize_query(query)
+        if reference_query is None:
+            reference_query = Query(target=q.target, evidence={}, do={})
+        rq = self._normalize_query(reference_query)
+        if rq.target != q.target:
+            raise ValueError("query and reference_query must have the same target node.")
+        qp, qs = self.infer_posterior(q, **kwargs)
+        rp, rs = self.infer_posterior(rq, **kwargs)
+        qst = self._posterior_stats(qp, qs, eps=eps)
+        rst = self._posterior_stats(rp, rs, eps=eps)
+        q_mean, r_mean = self._broadcast_batch(qst["mean"], rst["mean"])
+        q_std, r_std = self._broadcast_batch(qst["std"], rst["std"])
+        q_ess, r_ess = self._broadcast_batch(qst["ess"], rst["ess"])
+        d_mean = q_mean - r_mean
+        d_std = q_std - r_std
+        return {
+            "target": q.target,
+            "query_stats": {"mean": q_mean, "std": q_std, "effective_sample_size": q_ess},
+            "reference_stats": {"mean": r_mean, "std": r_std, "effective_sample_size": r_ess},
+            "delta_mean": d_mean,
+            "delta_std": d_std,
+            "relative_mean_change": d_mean / r_mean.abs().clamp_min(eps),
+            "relative_std_change": d_std / r_std.abs().clamp_min(eps),
+        }
+
     def _tensor(self, v) -> torch.Tensor:
         t = v.to(device=self.device, dtype=torch.float32) if isinstance(v, torch.Tensor) else \
             torch.tensor(v, device=self.device, dtype=torch.float32)

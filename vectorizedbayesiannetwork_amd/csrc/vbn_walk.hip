@@ -1533,6 +1533,53 @@ __global__ void __launch_bounds__(RB_THREADS) vbn_rb_epilogue_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// weighted posterior summary (vbn.py:483-504): one 256-thread workgroup per query, two passes
+// over the query's S particles (mean, then the centred second moment as the reference does).
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(RB_THREADS) vbn_posterior_stats_kernel(
+    const float* __restrict__ pdf, const float* __restrict__ x, float* __restrict__ mean,
+    float* __restrict__ stdv, float* __restrict__ ess, int S, int D, float eps) {
+#pragma clang fp contract(off)
+  __shared__ float red[RB_THREADS / WAVE];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* pr = pdf + b * S;
+  const float* xr = x + b * (int64_t)S * D;
+  auto wraw = [&](int s) {
+    const float v = pr[s];
+    return (v != v || v == INFINITY || v == -INFINITY) ? 0.f : fmaxf(v, 0.f);
+  };
+  float a = 0.f;
+  for (int s = tid; s < S; s += RB_THREADS) a += wraw(s);
+  const float denom = block_sum(a, red);
+  const bool ok = denom > eps;
+  const float dn = fmaxf(denom, eps), uni = 1.0f / (float)max(1, S);
+  auto wt = [&](int s) { return ok ? wraw(s) / dn : uni; };
+  float q = 0.f;
+  for (int s = tid; s < S; s += RB_THREADS) {
+    const float w = wt(s);
+    q += w * w;
+  }
+  const float sq = block_sum(q, red);
+  if (tid == 0) ess[b] = 1.0f / fmaxf(sq, eps);
+  for (int d = 0; d < D; ++d) {
+    float m = 0.f;
+    for (int s = tid; s < S; s += RB_THREADS) m += wt(s) * xr[(int64_t)s * D + d];
+    const float mu = block_sum(m, red);
+    float v = 0.f;
+    for (int s = tid; s < S; s += RB_THREADS) {
+      const float c = xr[(int64_t)s * D + d] - mu;
+      v += wt(s) * (c * c);
+    }
+    const float var = block_sum(v, red);
+    if (tid == 0) {
+      mean[b * D + d] = mu;
+      stdv[b * D + d] = sqrtf(fmaxf(var, 0.f));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // C-ABI
 // ------------------------------------------------------------------------------------------
 static thread_local char g_err[512];
@@ -1585,6 +1632,17 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
     case 31u: hipLaunchKernelGGL(vbn_walk_kernel<31u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
     default: hipLaunchKernelGGL(vbn_walk_kernel<63u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
   }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  return 0;
+}
+
+extern "C" int vbn_hip_posterior_stats(const float* pdf, const float* x, float* mean, float* std, float* ess,
+                                       int64_t n_queries, int32_t n_samples, int32_t dim, float eps, void* stream) {
+  if (!pdf || !x || !mean || !std || !ess || n_queries <= 0 || n_samples <= 0 || dim <= 0)
+    return fail(VBN_E_ARGS, "vbn_hip_posterior_stats: bad arguments");
+  hipLaunchKernelGGL(vbn_posterior_stats_kernel, dim3((unsigned)n_queries), dim3(RB_THREADS), 0,
+                     (hipStream_t)stream, pdf, x, mean, std, ess, n_samples, dim, eps);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;

@@ -501,8 +501,9 @@ class ResampledImportanceSampling(_EngineBase):
         threshold = max(1.0, thr_in * float(n)) if thr_in <= 1.0 else thr_in            # 62-65
         self._last_resampled = False
         order = [x for x in model.topo]                                                 # plan order
-        cuts = [i + 1 for i, x in enumerate(order) if x in ev] if resample else []      # 75-90
-        cuts = [c for c in cuts if c < len(order)] + [len(order)]
+        # a segment ends after every evidence node (ESS check, 75-90); the last segment may be
+        # empty when the last node is evidence (it only reloads the state and writes outputs)
+        cuts = ([i + 1 for i, x in enumerate(order) if x in ev] if resample else []) + [len(order)]
         if len(cuts) == 1:
             log_w, xs = run_walk(pk, plan, fx, b, n, seed=seed, q_base=self.q_base, noise=noise)
         else:

@@ -5,6 +5,7 @@
 * ``vbn_hip::normalize_weights``  -> ``vbn_hip_normalize_weights`` (softmax over S + ESS)
 * ``vbn_hip::rb_epilogue``        -> ``vbn_hip_rb_epilogue``       (Rao-Blackwellized target)
 * ``vbn_hip::resample``           -> ``vbn_hip_resample``          (multinomial particle resampling)
+* ``vbn_hip::posterior_stats``    -> ``vbn_hip_posterior_stats``   (weighted mean / std / ESS)
 
 Both run asynchronously on the current HIP stream, allocate fresh contiguous outputs and
 have fake (meta) implementations for shape inference.  Host-side checks make sure every
@@ -21,7 +22,7 @@ from torch import Tensor
 from . import _lib
 from .plan import STEP_INTS
 
-__all__ = ["walk", "walk_segment", "normalize_weights", "rb_epilogue", "resample"]
+__all__ = ["walk", "walk_segment", "normalize_weights", "rb_epilogue", "resample", "posterior_stats"]
 
 
 def _ptr(t: Optional[Tensor]) -> Optional[int]:
@@ -233,3 +234,29 @@ def resample(w: Tensor, u: Optional[Tensor], seed: int, offset: int, q_base: int
 @resample.register_fake
 def _resample_fake(w, u, seed, offset, q_base, state_in, state_out):
     return None
+
+
+@torch.library.custom_op("vbn_hip::posterior_stats", mutates_args=())
+def posterior_stats(pdf: Tensor, samples: Tensor, eps: float) -> Tuple[Tensor, Tensor, Tensor]:
+    """pdf [B,S], samples [B,S,D] -> (mean [B,D], std [B,D], ess [B]) (vbn.py:483-504)."""
+    if pdf.device.type != "cuda" or pdf.dim() != 2 or samples.dim() != 3:
+        raise ValueError("vbn_hip::posterior_stats: pdf [B,S] and samples [B,S,D] GPU tensors expected")
+    b, s = pdf.shape
+    d = samples.shape[2]
+    pdf = pdf.to(torch.float32).contiguous()
+    samples = samples.to(device=pdf.device, dtype=torch.float32).contiguous()
+    mean = torch.empty(b, d, device=pdf.device, dtype=torch.float32)
+    std = torch.empty_like(mean)
+    ess = torch.empty(b, device=pdf.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(pdf.device):
+        _lib.check(lib.vbn_hip_posterior_stats(
+            _ptr(pdf), _ptr(samples), _ptr(mean), _ptr(std), _ptr(ess), b, s, d, float(eps),
+            ctypes.c_void_p(_stream_handle(pdf.device))), "vbn_hip_posterior_stats")
+    return mean, std, ess
+
+
+@posterior_stats.register_fake
+def _posterior_stats_fake(pdf, samples, eps):
+    b, d = pdf.shape[0], samples.shape[2]
+    return pdf.new_empty(b, d), pdf.new_empty(b, d), pdf.new_empty(b)
