@@ -1,5 +1,5 @@
-"""MI355X-native batched Bayesian-network inference (drop-in for VBN's MCM / IS / LW /
-ancestral path and the gaussian_nn / linear_gaussian / mdn / kde / softmax_nn CPDs).
+"""MI355X-native batched Bayesian-network inference (drop-in for VBN's MCM / IS / LW / RB /
+RIS / ancestral path and the gaussian_nn / linear_gaussian / mdn / kde / softmax_nn CPDs).
 
 Importing the package does not touch the GPU; the HIP library is loaded on first use and
 the accelerated entry points raise if it is missing (there is no CPU fallback).
@@ -11,6 +11,8 @@ from .engines import (  # noqa: F401
     LikelihoodWeighting,
     MonteCarloMarginalization,
     Query,
+    RaoBlackwellizedMarginalization,
+    ResampledImportanceSampling,
 )
 from .model import BNModel, CPDRecord, model_from_checkpoint, model_from_vbn, random_init_model  # noqa: F401
 from .api import VBN, ConfigItem, defaults  # noqa: F401

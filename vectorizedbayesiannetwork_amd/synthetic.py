@@ -76,8 +76,8 @@ CONFIGS = {
                  kde_max_points=10000),
     "cfg5": dict(name="128node-mixed-mcm", n_nodes=128,
                  kinds=("gaussian_nn", "linear_gaussian", "mdn", "kde", "softmax_nn"),
-                 engine="monte_carlo_marginalization", B=65536, S=2048, rows=8192,
-                 kde_max_points=4096),
+                 engine="monte_carlo_marginalization", B=8192, S=2048, rows=8192,
+                 kde_max_points=4096),           # B per GPU: 65,536 queries over 8 MI355X
     # §8(f) row on the cfg2 DAG: Rao-Blackwellized target (P = S = 1024)
     "rb32": dict(name="32node-gaussian_nn-rb", n_nodes=32, kinds=("gaussian_nn",),
                  engine="rao_blackwellized_marginalization", B=4096, S=1024, rows=2048),
