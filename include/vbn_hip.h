@@ -25,6 +25,9 @@
  *                             SoftmaxNNCPD    (vbn/cpds/softmax_nn.py:581-759).
  *   vbn_hip_posterior_stats VBN._posterior_stats (vbn/vbn.py:483-504), the summary behind
  *                             VBN.infer_relative (vbn/vbn.py:519-568)
+ *   vbn_hip_walk (mode GIBBS)  GibbsSampler.sample sweeps (vbn/sampling/gibbs.py:23-92):
+ *                             8 candidates per chain drawn by the node's CPD, scored with the
+ *                             node's and its children's log-probs, one chosen per chain
  *   vbn_hip_resample        the multinomial resampling step of
  *                             ResampledImportanceSampling._resample
  *                               (vbn/inference/resampled_importance_sampling.py:33-41)
@@ -44,7 +47,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 3
+#define VBN_ABI_VERSION 4
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001
@@ -64,9 +67,12 @@ enum vbn_role {
   VBN_ROLE_SKIP = 0,
   VBN_ROLE_LATENT = 1,
   VBN_ROLE_FIXED = 2,
-  VBN_ROLE_PARAMS = 3   /* write the CPD's conditional parameters, no draw (RB target):
+  VBN_ROLE_PARAMS = 3,  /* write the CPD's conditional parameters, no draw (RB target):
                            gaussian_nn / linear_gaussian: loc[D] ++ scale[D];
                            softmax_nn (D = 1): class probabilities[C]                   */
+  VBN_ROLE_SELECT = 4,  /* Gibbs: softmax over the 8 candidate lanes of a chain, choose one,
+                           broadcast its value (out_col, out_dim) to the chain's lanes     */
+  VBN_ROLE_COLLECT = 5  /* Gibbs: after burn-in, every thin-th sweep, write the target     */
 };
 
 /* step flags */
@@ -77,6 +83,8 @@ enum vbn_role {
 #define VBN_F_CLIP 16       /* softmax_nn within_bin_clip                                      */
 #define VBN_F_F32L2 32      /* NN CPD: exact f32 MFMA chain for layer 2 instead of split-f16   */
 #define VBN_F_KDE_VALU 64   /* kde: pairwise distances on packed VALU (else the 16x16x4 f32 MFMA tile) */
+#define VBN_F_KEEP 128      /* fixed role: the value is already in the node's slot (Gibbs)      */
+#define VBN_F_LPRESET 256   /* reset the particle's log-prob accumulator before this step       */
 
 /* activations of the NN CPDs (reference gaussian_nn.py:19-24) */
 enum vbn_act { VBN_ACT_RELU = 0, VBN_ACT_TANH = 1, VBN_ACT_GELU = 2, VBN_ACT_ELU = 3 };
@@ -88,7 +96,9 @@ enum vbn_within { VBN_WITHIN_UNIFORM = 0, VBN_WITHIN_TRIANGULAR = 1, VBN_WITHIN_
 enum vbn_mode {
   VBN_MODE_MCM = 0,       /* out_lp = exp(lp)          (pdf)          */
   VBN_MODE_WEIGHTED = 1,  /* out_lp = lp               (log-weights)  */
-  VBN_MODE_SAMPLE = 2     /* no out_lp                                */
+  VBN_MODE_SAMPLE = 2,    /* no out_lp                                */
+  VBN_MODE_GIBBS = 3      /* gibbs_iters sweeps over the step table; lane = (chain, candidate),
+                             n_samples = 8 candidates; out_x = [B][n_collect][n_out_cols]    */
 };
 
 /* One node of the topological walk (32 x int32, filled by the host plan packer). */
@@ -131,7 +141,10 @@ typedef struct vbn_walk_args {
                               segments (resampled importance sampling)                 */
   int32_t state_flags;     /* 1: load slots + log-weight from state before the first step;
                               2: store them after the last step                        */
-  int32_t reserved_args;
+  int32_t gibbs_iters;     /* Gibbs sweeps (mode GIBBS; burn_in + n_collect * thin)   */
+  int32_t gibbs_burn_in;
+  int32_t gibbs_thin;
+  int32_t n_noise;         /* noise nodes per sweep (injected-noise stride, mode GIBBS) */
 } vbn_walk_args;
 
 int vbn_hip_abi_version(void);

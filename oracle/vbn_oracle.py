@@ -823,3 +823,51 @@ def posterior_stats(pdf: torch.Tensor, samples: torch.Tensor, eps: float = 1e-12
     std = var.clamp_min(0.0).sqrt()
     ess = 1.0 / (weights ** 2).sum(dim=1).clamp_min(eps)
     return {"mean": mean, "std": std, "ess": ess}
+
+
+# ----------------------------------------------------------------------------------------
+# Gibbs sampler (reference vbn/sampling/gibbs.py)
+# ----------------------------------------------------------------------------------------
+
+def gibbs(model: BNModel, target: str, evidence: Dict, do: Dict, n_samples: int, draws,
+          burn_in: int = 10, n_steps: int = 1, n_candidates: int = 8) -> torch.Tensor:
+    """GibbsSampler.sample (gibbs.py:23-92): candidate-reweighting sweeps over the latent
+    nodes, started from one ancestral draw (29); returns ``[b, n_samples, Dt]``."""
+    b = _batch(evidence, do)
+    fixed = _fixed(evidence, do)
+    cols, total = _layout(model)
+    current = torch.zeros(b, 1, total)                                   # ancestral.py:13-38, n=1
+    for node in model.topo:
+        if node in fixed:
+            current[..., cols[node]] = fixed[node].unsqueeze(1)
+            continue
+        current[..., cols[node]] = cpd_sample(model.cpds[node], _gather_parents(model, node, current, cols), 1,
+                                              draws)
+    latent = [nd for nd in model.topo if nd not in fixed]                # 30-32
+    children = model.children()
+    thin = max(n_steps, 1)
+    collected = []
+    for step in range(burn_in + n_samples * thin):                       # 34-35
+        for node in latent:
+            pt = _gather_parents(model, node, current, cols)             # 38-45
+            if pt is not None and pt.shape[1] != n_candidates:
+                pt = pt.expand(b, n_candidates, -1)
+            rec = model.cpds[node]
+            cand = cpd_sample(rec, pt, n_candidates, draws)              # 50
+            score = cpd_log_prob(rec, cand, pt)                          # 51
+            for ch in children[node]:                                    # 52-78
+                cv = current[..., cols[ch]].expand(b, n_candidates, -1)
+                parts = [cand if p == node else current[..., cols[p]].expand(b, n_candidates, -1)
+                         for p in model.parents[ch]]
+                score = score + cpd_log_prob(model.cpds[ch], cv, torch.cat(parts, dim=-1) if parts else None)
+            w = torch.softmax(score, dim=1)                              # 79
+            choice = draws.categorical(w)                                # 80
+            chosen = cand[torch.arange(b), choice]                       # 81
+            current[..., cols[node]] = chosen.unsqueeze(1)               # 82
+        if step >= burn_in and (step - burn_in) % thin == 0:             # 83-87
+            # a view of ``current`` (no copy): later sweeps overwrite it in place, so every
+            # collected entry ends up holding the final sweep's value, as in the reference
+            collected.append(current[..., cols[target]])
+    if not collected:
+        return current[..., cols[target]]
+    return torch.cat(collected, dim=1)

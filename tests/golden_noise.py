@@ -41,3 +41,43 @@ def resample_uniforms(case: dict):
     """The engine-level multinomial resampling draws (node None), in order: list of [B, S]."""
     S = int(case["n_samples"])
     return [r["value"].float().view(-1, S) for r in case["draws"] if r["node"] is None and r["kind"] == "cat"]
+
+
+def gibbs_noise(case: dict, model, latent, dmax: int):
+    """Recorded draws of a Gibbs fixture -> (initial-walk noise dict, sweep noise tensor).
+
+    Phase 0 is the initial ancestral draw (S = 1); phase 1 holds, per sweep and latent node,
+    the node's 8-candidate draws then the chain choice (a ``cat`` record with node None,
+    whose CDF midpoint is the injected uniform).  Sweep layout [iters, 2L, 2, B, 8, dmax]:
+    candidate draws at index 2j, the choice uniform at 2j + 1 (slot 0, candidate 0, dim 0).
+    """
+    init = noise_dict({**case, "n_samples": 1, "draws": [r for r in case["draws"] if r["phase"] == 0]}, model, 0)
+    B = int(next(iter(case["query"]["evidence"].values())).shape[0]) if case["query"]["evidence"] else 1
+    if case["query"]["do"]:
+        B = int(next(iter(case["query"]["do"].values())).shape[0])
+    thin = max(int(case["params"]["n_steps"]), 1)
+    iters = int(case["params"]["burn_in"]) + int(case["n_samples"]) * thin
+    L = len(latent)
+    out = torch.zeros(iters, max(2 * L, 1), 2, B, 8, dmax)
+    recs = [r for r in case["draws"] if r["phase"] == 1]
+    pos = 0
+    for it in range(iters):
+        for j, node in enumerate(latent):
+            D = model.out_dim(node)
+            per_dim0 = model.cpds[node].kind == "softmax_nn"
+            while recs[pos]["node"] == node:
+                r = recs[pos]
+                pos += 1
+                v = r["value"].float()
+                bq = v.numel() // (8 * D) if (r["kind"] not in ("cat", "randint") or per_dim0) else v.numel() // 8
+                if r["kind"] in ("cat", "randint"):
+                    vv = v.view(bq, 8, D) if per_dim0 else v.view(bq, 8, 1)
+                    out[it, 2 * j, 0, :, :, :vv.shape[-1]] = vv.expand(B, 8, vv.shape[-1])
+                else:
+                    out[it, 2 * j, 1, :, :, :D] = v.view(bq, 8, D).expand(B, 8, D)
+            r = recs[pos]
+            pos += 1
+            assert r["node"] is None and r["kind"] == "cat", r["kind"]
+            out[it, 2 * j + 1, 0, :, 0, 0] = r["value"].float().view(-1).expand(B)
+    assert pos == len(recs)
+    return init, out

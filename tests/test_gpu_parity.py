@@ -71,7 +71,7 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
     model, vbn = _vbn(fx)
     eng = case["engine"]
     n = case["n_samples"]
-    nd0 = noise_dict(case, model, 0)
+    nd0 = noise_dict(case, model, 0) if eng != "gibbs" else None
     if eng == "cpd":
         node = case["node"]
         rec = model.cpds[node]
@@ -145,6 +145,16 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
         assert (e._last_reason or "") == (reason or "")
         _close("samples", xs, rxs, S_ATOL, S_RTOL)
         _close("pdf", pdf, rpdf, P_ATOL, P_RTOL)
+    elif eng == "gibbs":
+        from golden_noise import gibbs_noise
+        from vectorizedbayesiannetwork_amd.engines import GibbsSampler
+        e = GibbsSampler(n_samples=n, kde_valu=kde_valu, **p)
+        pk_latent = [x for x in model.topo if x not in q["evidence"] and x not in q["do"]]
+        noise = gibbs_noise(case, model, pk_latent, max(model.out_dim(x) for x in model.topo))
+        xs = e.sample(vbn, qq, n, _noise=noise)
+        rxs = O.gibbs(model, q["target"], q["evidence"], q["do"], n, draws, **p)
+        _close("samples", xs, rxs, S_ATOL, S_RTOL)
+        _close("samples(reference)", xs, case["outputs"]["samples"], S_ATOL, S_RTOL)
     else:
         raise AssertionError(eng)
 

@@ -46,6 +46,9 @@ def _run_case(model, case):
         if reason:                               # fallback engine: likelihood_weighting
             pdf, xs = O.likelihood_weighting(model, q["target"], q["evidence"], q["do"], n, draws)
         out = {"pdf": pdf, "samples": xs, "fallback": bool(reason), "reason": reason or ""}
+    elif eng == "gibbs":
+        out = {"samples": O.gibbs(model, q["target"], q["evidence"], q["do"], n, draws,
+                                  burn_in=p["burn_in"], n_steps=p["n_steps"])}
     else:
         raise AssertionError(eng)
     assert draws.exhausted(), "oracle consumed fewer draws than the reference"

@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -57,7 +57,10 @@ class VbnWalkArgs(ctypes.Structure):
         ("offset", ctypes.c_uint64),
         ("state", ctypes.c_void_p),
         ("state_flags", ctypes.c_int32),
-        ("reserved_args", ctypes.c_int32),
+        ("gibbs_iters", ctypes.c_int32),
+        ("gibbs_burn_in", ctypes.c_int32),
+        ("gibbs_thin", ctypes.c_int32),
+        ("n_noise", ctypes.c_int32),
     ]
 
 

@@ -30,7 +30,7 @@ __all__ = ["VBN", "ConfigItem", "defaults"]
 
 
 # Packaged defaults of the in-scope engines (reference vbn/configs/inference/*.yaml,
-# vbn/configs/sampling/ancestral.yaml).
+# vbn/configs/sampling/{ancestral,gibbs}.yaml).
 _ENGINE_DEFAULTS = {
     "inference": {
         "monte_carlo_marginalization": {"n_samples": 1024},
@@ -41,7 +41,8 @@ _ENGINE_DEFAULTS = {
         "resampled_importance_sampling": {"n_samples": 1024, "ess_threshold": 0.5, "resample": True,
                                           "clamp_obs": True},
     },
-    "sampling": {"ancestral": {"n_samples": 512}},
+    "sampling": {"ancestral": {"n_samples": 512},
+                 "gibbs": {"n_samples": 512, "burn_in": 50, "n_steps": 5}},
 }
 
 

@@ -106,8 +106,10 @@ struct Lane {
   float* scr;    // LDS [max_out][64]
   int lane;
   int64_t p;     // particle (clamped)
-  int64_t b;     // query
-  int s;         // sample
+  int64_t b;     // query (Gibbs: chain)
+  int s;         // sample (Gibbs: candidate)
+  int iter;      // Gibbs sweep (0 for every other walk)
+  bool valid;    // particle index inside the batch
 };
 
 // Draws of node ``st``, dimension d, for this particle.  Stream 0 gives a standard normal
@@ -120,14 +122,17 @@ __device__ __forceinline__ uint2 rng_words(const vbn_walk_args& A, const vbn_ste
   const uint32_t qkey = (st.flags & VBN_F_SHARED) ? 0u : (uint32_t)(A.q_base + L.b + 1);
   const uint32_t sid = ((uint32_t)(A.offset & 0xffu) << 24) |
                        (((uint32_t)st.node_id * 16u + (uint32_t)d) * 2u + (uint32_t)stream);
-  return philox2x32(make_uint2((uint32_t)L.s, qkey ^ (uint32_t)(A.seed >> 32)), (uint32_t)A.seed + sid);
+  const uint32_t ctr = (uint32_t)L.s + (uint32_t)L.iter * (uint32_t)A.n_samples;
+  return philox2x32(make_uint2(ctr, qkey ^ (uint32_t)(A.seed >> 32)), (uint32_t)A.seed + sid);
 }
 
 __device__ __forceinline__ int64_t noise_index(const vbn_walk_args& A, const vbn_step& st, int d, int slot,
                                                const Lane& L) {
   const int64_t bq = A.noise_b == 1 ? 0 : L.b;
   const int64_t stride_slot = (int64_t)A.noise_b * A.n_samples * A.dmax;
-  return ((int64_t)st.noise_idx * 2 + slot) * stride_slot + (bq * A.n_samples + L.s) * A.dmax + d;
+  const int64_t stride_iter = (int64_t)A.n_noise * 2 * stride_slot;       // Gibbs sweeps
+  return (int64_t)L.iter * stride_iter + ((int64_t)st.noise_idx * 2 + slot) * stride_slot +
+         (bq * A.n_samples + L.s) * A.dmax + d;
 }
 
 __device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
@@ -150,6 +155,12 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
                                              const Lane& L) {
   const int64_t row = A.fixed_per_particle ? L.p : L.b;
   return A.fixed[row * A.fixed_ld + st.fixed_col + d];
+}
+
+// value of a fixed node: from the fixed buffer, or (VBN_F_KEEP, Gibbs) the slot's current value
+__device__ __forceinline__ float node_fixed(const vbn_walk_args& A, const vbn_step& st, int d,
+                                            const Lane& L) {
+  return (st.flags & VBN_F_KEEP) ? vread(L, st.out_col + d) : fixed_value(A, st, d, L);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -418,7 +429,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
         x = draw_normal(A, st, d, L) * scale + loc;  // torch.normal(loc, scale)
         vwrite(L, st.out_col + d, x);
       } else {
-        x = fixed_value(A, st, d, L);
+        x = node_fixed(A, st, d, L);
         vwrite(L, st.out_col + d, x);
       }
       if (want_lp) {                                 // Normal.log_prob (gaussian_nn.py:276-279)
@@ -446,7 +457,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
     if (latent) {
       x = loc + draw_normal(A, st, d, L) * scale;
     } else {
-      x = fixed_value(A, st, d, L);
+      x = node_fixed(A, st, d, L);
     }
     vwrite(L, st.out_col + d, x);
     if (want_lp) {
@@ -485,7 +496,7 @@ __device__ __forceinline__ void step_linear_gaussian(const vbn_walk_args& A, con
     if (latent) {
       x = loc + draw_normal(A, st, d, L) * scale[d];
     } else {
-      x = fixed_value(A, st, d, L);
+      x = node_fixed(A, st, d, L);
     }
     vwrite(L, st.out_col + d, x);
     if (st.flags & VBN_F_LOGP) {
@@ -558,7 +569,7 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
     for (int d = 0; d < D; ++d)
       vwrite(L, st.out_col + d, loc_kd(idx, d) + draw_normal(A, st, d, L) * scale_kd(idx, d));
   } else {
-    for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
+    for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, node_fixed(A, st, d, L));
   }
   if (want_lp) {
     // logsumexp_k(log pi_k + log N_k(x))  (mdn.py:263-272), online form
@@ -657,7 +668,7 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
         x = cont;
       }
     } else {
-      x = fixed_value(A, st, d, L);
+      x = node_fixed(A, st, d, L);
     }
     vwrite(L, st.out_col + d, x);
     if (st.flags & VBN_F_LOGP) {
@@ -1180,7 +1191,7 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
       vwrite(L, st.out_col + d, sel + draw_normal(A, st, d, L) * noise_scale);
     }
   } else {
-    for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
+    for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, node_fixed(A, st, d, L));
   }
 
   if ((st.flags & VBN_F_LOGP) && st.reserved[2] >= 0 && (root || st.reserved[1] >= 0)) {
@@ -1246,6 +1257,45 @@ __device__ __forceinline__ void step_kde(const vbn_walk_args& A, const vbn_step&
 }
 
 // ------------------------------------------------------------------------------------------
+// Gibbs sweep steps (gibbs.py:40-87): lanes 8c .. 8c+7 hold chain c's 8 candidates
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void gibbs_select(const vbn_walk_args& A, const vbn_step& st, Lane& L, float lp) {
+  const int lane = L.lane, g0 = lane & ~7;
+  float m = fmaxf(lp, __shfl_xor(lp, 1));
+  m = fmaxf(m, __shfl_xor(m, 2));
+  m = fmaxf(m, __shfl_xor(m, 4));
+  const float e = __expf(lp - m);                       // softmax(log_score, 1) (79)
+  float se = e + __shfl_xor(e, 1);
+  se += __shfl_xor(se, 2);
+  se += __shfl_xor(se, 4);
+  float pk[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) pk[k] = __shfl(e, g0 + k) / se;
+  // one uniform per chain (candidate lane 0's draw), multinomial(weights, 1) (80)
+  // (without injected noise the draw uses dimension stream 15 of the node, which no candidate
+  // draw of a node with fewer than 16 dims touches)
+  const int s_keep = L.s;
+  L.s = 0;
+  const float u = A.noise ? draw_uniforms(A, st, 0, L).x : u01(rng_words(A, st, 15, 1, L).x);
+  L.s = s_keep;
+  const int idx = inv_cdf(8, u, [&](int k) { return pk[k]; });
+  for (int d = 0; d < st.out_dim; ++d) {
+    const float v = __shfl(vread(L, st.out_col + d), g0 + idx);
+    wave_sync();
+    vwrite(L, st.out_col + d, v);                        // chosen candidate (81-82)
+  }
+}
+
+__device__ __forceinline__ void gibbs_collect(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  const int it = L.iter, burn = A.gibbs_burn_in, thin = max(A.gibbs_thin, 1);
+  if (it < burn || (it - burn) % thin != 0 || L.s != 0 || !L.valid) return;     // 83-87
+  const int n_collect = (A.gibbs_iters - burn + thin - 1) / thin;
+  const int k = (it - burn) / thin;
+  for (int d = 0; d < st.out_dim; ++d)
+    A.out_x[(L.b * n_collect + k) * A.n_out_cols + d] = vread(L, st.out_col + d);
+}
+
+// ------------------------------------------------------------------------------------------
 // the walk
 // ------------------------------------------------------------------------------------------
 // KM: bit0 gaussian_nn, bit1 linear_gaussian, bit2 mdn, bit3 kde, bit4 softmax_nn,
@@ -1268,6 +1318,8 @@ __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) 
   L.p = valid ? p_raw : total - 1;
   L.b = L.p / A.n_samples;
   L.s = (int)(L.p - L.b * A.n_samples);
+  L.iter = 0;
+  L.valid = valid;
 
   float lp = 0.f;
   if (A.state && (A.state_flags & 1)) {             // resume a segmented walk
@@ -1275,11 +1327,24 @@ __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) 
     lp = A.state[(int64_t)A.n_slots * total + L.p];
     wave_sync();
   }
+  const int iters = A.mode == VBN_MODE_GIBBS ? A.gibbs_iters : 1;
+  for (int it = 0; it < iters; ++it) {
+  L.iter = it;
   for (int i = 0; i < A.n_steps; ++i) {
     const vbn_step st = steps[i];
     if (st.role == VBN_ROLE_SKIP) continue;
+    if (st.flags & VBN_F_LPRESET) lp = 0.f;
+    if (st.role == VBN_ROLE_SELECT) {
+      gibbs_select(A, st, L, lp);
+      wave_sync();
+      continue;
+    }
+    if (st.role == VBN_ROLE_COLLECT) {
+      gibbs_collect(A, st, L);
+      continue;
+    }
     if (st.role == VBN_ROLE_FIXED && !(st.flags & VBN_F_LOGP)) {   // evidence / do: value only
-      for (int d = 0; d < st.out_dim; ++d) vwrite(L, st.out_col + d, fixed_value(A, st, d, L));
+      for (int d = 0; d < st.out_dim; ++d) vwrite(L, st.out_col + d, node_fixed(A, st, d, L));
       wave_sync();
       continue;
     }
@@ -1292,7 +1357,9 @@ __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) 
     }
     wave_sync();
   }
+  }
   if (!valid) return;
+  if (A.mode == VBN_MODE_GIBBS) return;                  // outputs written by COLLECT steps
   if (A.state && (A.state_flags & 2)) {
     for (int c = 0; c < A.n_slots; ++c) A.state[(int64_t)c * total + L.p] = vread(L, c);
     A.state[(int64_t)A.n_slots * total + L.p] = lp;
@@ -1608,6 +1675,10 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
     return fail(VBN_E_ARGS, "vbn_hip_walk: out_x without out_cols");
   const int64_t lds = vbn_hip_lds_bytes(a->n_slots, a->max_out);
   if (lds > 160 * 1024) return fail(VBN_E_LDS, "vbn_hip_walk: plan needs more than 160 KiB of LDS per wave");
+  if (a->mode == VBN_MODE_GIBBS &&
+      (a->n_samples != 8 || a->gibbs_iters <= 0 || a->gibbs_burn_in < 0 || a->gibbs_burn_in >= a->gibbs_iters ||
+       a->gibbs_thin <= 0 || !a->out_x || (a->noise && a->n_noise <= 0)))
+    return fail(VBN_E_ARGS, "vbn_hip_walk: Gibbs walk needs 8 candidates, iters > burn_in >= 0, thin > 0, out_x");
   const int64_t total = a->n_queries * (int64_t)a->n_samples;
   const int64_t blocks = (total + WAVE - 1) / WAVE;
   if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");

@@ -40,8 +40,8 @@ import torch
 
 from . import ops
 from .model import BNModel, model_from_vbn
-from .plan import (MODE_MCM, MODE_SAMPLE, MODE_WEIGHTED, PackedModel, QueryPlan, barren_pruned,
-                   build_plan)
+from .plan import (MODE_MCM, MODE_SAMPLE, MODE_WEIGHTED, GibbsPlan, PackedModel, QueryPlan, barren_pruned,
+                   build_gibbs_plan, build_plan)
 from .registry import register_inference, register_sampling
 
 __all__ = [
@@ -561,3 +561,80 @@ class AncestralSampler(_EngineBase):
             out[node] = xs[..., c:c + d]
             c += d
         return out
+
+
+@register_sampling("gibbs")
+class GibbsSampler(_EngineBase):
+    """sampling/gibbs.py:12-92 on the GPU: one ancestral walk for the start state (29), then
+    every sweep of every chain in one launch (lanes = chain x 8 candidates, gibbs.py:36-87).
+
+    ``collect="reference"`` (default) returns what the reference returns: its ``collected``
+    list holds views of the chain state (gibbs.py:86), so every entry is the state after the
+    LAST sweep; the walk then writes only that sweep.  ``collect="chain"`` writes the target
+    at every collected sweep instead (burn-in, thinning by ``n_steps``) -- the Markov chain.
+    """
+
+    def __init__(self, n_samples: int = 200, burn_in: int = 10, n_steps: int = 1, collect: str = "reference",
+                 **kwargs):
+        super().__init__(n_samples=n_samples, **kwargs)
+        self.burn_in = int(burn_in)
+        self.n_steps = int(n_steps)
+        self.n_candidates = 8
+        if collect not in ("reference", "chain"):
+            raise ValueError(f"collect must be 'reference' or 'chain', got {collect!r}")
+        self.collect = collect
+
+    def _gibbs_plan(self, pk: PackedModel, target: str, vals) -> GibbsPlan:
+        model = pk.model
+        ck = ("gibbs", target, tuple(sorted(vals)), self.exact_f32, self.kde_valu)
+        gp = model._cache.get(ck)
+        if gp is None:
+            gp = build_gibbs_plan(pk, latent=[x for x in model.topo if x not in vals],
+                                  fixed=[x for x in model.topo if x in vals], target=target,
+                                  exact_f32=self.exact_f32, kde_valu=self.kde_valu)
+            model._cache[ck] = gp
+        return gp
+
+    def sample(self, vbn, query, n_samples: Optional[int] = None, **kwargs):
+        n = int(n_samples or self.n_samples)
+        target, ev, do = self._query(query)
+        if not target:
+            raise ValueError("Gibbs sampling needs a query target")
+        b = infer_batch_size(ev, do)
+        dev = _device_of(vbn)
+        pk = packed_model(vbn, dev)
+        model = pk.model
+        if target not in model.cpds:
+            raise ValueError(f"Unknown target node: {target}")
+        vals = _fixed_values(query, dev)
+        _check_discrete(pk, vals, list(ev))
+        gp = self._gibbs_plan(pk, target, vals)
+        init = gp.init
+        fx = _fixed_buffer(init, vals, b, dev)
+        seed = self._seed(kwargs)
+        init_noise, sweep_noise = kwargs.get("_noise") or (None, None)
+        state = torch.empty(init.n_slots + 1, b, device=dev, dtype=torch.float32)
+        _, x0 = run_walk(pk, init, fx, b, 1, seed=seed, q_base=self.q_base, noise=init_noise,
+                         state=state, state_flags=2)                                    # gibbs.py:29
+        thin = max(self.n_steps, 1)
+        iters = self.burn_in + n * thin                                                 # 34
+        slot, dt = init.slot_of[target], model.out_dim(target)
+        if iters == 0:
+            return x0[..., slot:slot + dt].contiguous()                                 # 89-91
+        if self.collect == "chain" and n > 0:
+            burn, th = self.burn_in, thin
+        else:
+            burn, th = iters - 1, 1                       # the final sweep (every collected view)
+        chains = state.view(init.n_slots + 1, b, 1).expand(-1, -1, 8).reshape(init.n_slots + 1, b * 8)
+        noise_b = b
+        if sweep_noise is not None:
+            sweep_noise = sweep_noise.to(device=dev, dtype=torch.float32).contiguous()
+            if sweep_noise.shape != (iters, gp.n_noise, 2, b, 8, pk.dmax):
+                raise ValueError(f"sweep noise must be [{iters}, {gp.n_noise}, 2, {b}, 8, {pk.dmax}]")
+        out = ops.gibbs_walk(gp.steps, gp.in_cols, pk.params, fx,
+                             sweep_noise, chains.contiguous(), b, init.n_slots, init.max_out, init.fixed_ld,
+                             noise_b, gp.n_noise, pk.dmax, dt, iters, burn, th, self.q_base, seed, 1,
+                             gp.kind_mask)
+        if self.collect == "chain" and n > 0:
+            return out
+        return out.expand(b, max(n, 1), dt).contiguous()

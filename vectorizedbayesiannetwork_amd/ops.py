@@ -20,7 +20,7 @@ import torch
 from torch import Tensor
 
 from . import _lib
-from .plan import STEP_INTS
+from .plan import MODE_GIBBS, STEP_INTS
 
 __all__ = ["walk", "walk_segment", "normalize_weights", "rb_epilogue", "resample", "posterior_stats"]
 
@@ -147,6 +147,79 @@ def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samp
     lp = params.new_empty(total if want_lp else 0)
     x = params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))
     return lp, x
+
+
+@torch.library.custom_op("vbn_hip::gibbs_walk", mutates_args=())
+def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: Optional[Tensor],
+               state: Tensor, n_queries: int, n_slots: int, max_out: int, fixed_ld: int, noise_b: int,
+               n_noise: int, dmax: int, out_dim: int, iters: int, burn_in: int, thin: int, q_base: int,
+               seed: int, offset: int, kind_mask: int) -> Tensor:
+    """``iters`` Gibbs sweeps (gibbs.py:34-87) over B chains x 8 candidate lanes, started from
+    ``state`` [n_slots + 1, B*8]; returns the collected target values [B, n_collect, out_dim]."""
+    device = params.device
+    if device.type != "cuda":
+        raise RuntimeError("vbn_hip::gibbs_walk runs on the GPU only (no CPU fallback); "
+                           f"params are on {device}")
+    for name, t, dt in (("steps", steps, torch.int32), ("in_cols", in_cols, torch.int32),
+                        ("params", params, torch.float32), ("fixed", fixed, torch.float32),
+                        ("state", state, torch.float32)):
+        _check_dev(name, t, dt, device)
+    if steps.dim() != 2 or steps.shape[1] != STEP_INTS:
+        raise ValueError("vbn_hip::gibbs_walk: steps must be [n_steps, 32]")
+    if iters <= 0 or not 0 <= burn_in < iters or thin <= 0 or out_dim <= 0:
+        raise ValueError("vbn_hip::gibbs_walk: need iters > burn_in >= 0, thin > 0, out_dim > 0")
+    total = n_queries * 8
+    if state.numel() < (n_slots + 1) * total:
+        raise ValueError(f"vbn_hip::gibbs_walk: state has {state.numel()} values, needs {(n_slots + 1) * total}")
+    if fixed.numel() < n_queries * fixed_ld:
+        raise ValueError(f"vbn_hip::gibbs_walk: fixed buffer needs {n_queries}x{fixed_ld} values")
+    if noise is not None:
+        _check_dev("noise", noise, torch.float32, device)
+        need = iters * n_noise * 2 * noise_b * 8 * dmax
+        if noise.numel() < need or noise_b not in (1, n_queries):
+            raise ValueError(f"vbn_hip::gibbs_walk: noise has {noise.numel()} values, needs {need}")
+    n_collect = (iters - burn_in + thin - 1) // thin
+    x = torch.empty((n_queries, n_collect, out_dim), device=device, dtype=torch.float32)
+    a = _lib.VbnWalkArgs()
+    a.steps = steps.data_ptr()
+    a.in_cols = _ptr(in_cols)
+    a.params = _ptr(params)
+    a.fixed = _ptr(fixed)
+    a.noise = _ptr(noise)
+    a.out_cols = _ptr(in_cols)            # unused by the Gibbs walk (COLLECT reads the target slots)
+    a.out_lp = None
+    a.out_x = _ptr(x)
+    a.n_queries = n_queries
+    a.n_samples = 8
+    a.n_steps = int(steps.shape[0])
+    a.state = _ptr(state)
+    a.state_flags = 1
+    a.n_slots = n_slots
+    a.max_out = max_out
+    a.fixed_ld = fixed_ld
+    a.fixed_per_particle = 0
+    a.noise_b = noise_b
+    a.dmax = dmax
+    a.n_out_cols = out_dim
+    a.mode = MODE_GIBBS
+    a.kind_mask = kind_mask
+    a.q_base = q_base
+    a.seed = seed & ((1 << 64) - 1)
+    a.offset = offset & ((1 << 64) - 1)
+    a.gibbs_iters = iters
+    a.gibbs_burn_in = burn_in
+    a.gibbs_thin = thin
+    a.n_noise = n_noise
+    lib = _lib.load()
+    with torch.cuda.device(device):
+        _lib.check(lib.vbn_hip_walk(ctypes.byref(a), ctypes.c_void_p(_stream_handle(device))), "vbn_hip_walk")
+    return x
+
+
+@gibbs_walk.register_fake
+def _gibbs_walk_fake(steps, in_cols, params, fixed, noise, state, n_queries, n_slots, max_out, fixed_ld,
+                     noise_b, n_noise, dmax, out_dim, iters, burn_in, thin, q_base, seed, offset, kind_mask):
+    return params.new_empty((n_queries, (iters - burn_in + thin - 1) // thin, out_dim))
 
 
 @torch.library.custom_op("vbn_hip::normalize_weights", mutates_args=())

@@ -28,11 +28,12 @@ from .model import BNModel, CPDRecord
 
 # ---- must match include/vbn_hip.h -------------------------------------------------------
 KIND_ID = {"gaussian_nn": 0, "linear_gaussian": 1, "mdn": 2, "kde": 3, "softmax_nn": 4}
-ROLE_SKIP, ROLE_LATENT, ROLE_FIXED, ROLE_PARAMS = 0, 1, 2, 3
+ROLE_SKIP, ROLE_LATENT, ROLE_FIXED, ROLE_PARAMS, ROLE_SELECT, ROLE_COLLECT = 0, 1, 2, 3, 4, 5
 F_LOGP, F_ROOT, F_SHARED, F_STANDARDIZE, F_CLIP, F_F32L2, F_KDE_VALU = 1, 2, 4, 8, 16, 32, 64
+F_KEEP, F_LPRESET = 128, 256
 ACT_ID = {"relu": 0, "tanh": 1, "gelu": 2, "elu": 3}
 WITHIN_ID = {"uniform": 0, "triangular": 1, "gaussian": 2}
-MODE_MCM, MODE_WEIGHTED, MODE_SAMPLE = 0, 1, 2
+MODE_MCM, MODE_WEIGHTED, MODE_SAMPLE, MODE_GIBBS = 0, 1, 2, 3
 STEP_INTS = 32
 (S_KIND, S_ROLE, S_FLAGS, S_ACT, S_NIN, S_INOFF, S_OUTCOL, S_OUTDIM, S_FIXEDCOL, S_K, S_NOUT,
  S_NODEID, S_NOISE, S_AUX0, S_AUX1, S_AUX2, S_OFF_STD, S_OFF_W1, S_OFF_W2, S_OFF_B2, S_OFF_W3,
@@ -500,3 +501,63 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         in_cols=t(in_cols), out_cols=t(out_cols), n_steps=len(order), n_slots=max(n_slots, 1),
         max_out=max_out, fixed_nodes=fixed_nodes, fixed_ld=max(c, 1), noise_nodes=noise_nodes,
         out_nodes=list(out_nodes), mode=mode, slot_of=slot_of, kind_mask=kind_mask)
+
+
+@dataclass
+class GibbsPlan:
+    init: QueryPlan            # ancestral start state (gibbs.py:29), every node kept in its own slots
+    steps: torch.Tensor        # int32 [n_steps, 32]: one sweep (device)
+    n_steps: int
+    latent: List[str]          # sweep order; candidate noise index 2j, choice noise index 2j + 1
+    target: str
+    n_noise: int
+    in_cols: torch.Tensor      # parent slots of every row (children read their parents too)
+    kind_mask: int
+
+
+def build_gibbs_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[str], target: str,
+                     exact_f32: bool = False, kde_valu: bool = False) -> GibbsPlan:
+    """One Gibbs sweep as a step table (GibbsSampler.sample, gibbs.py:36-87).
+
+    Per latent node, in topological order: a LATENT step draws the chain's 8 candidates into
+    the node's slot (one per lane) and starts the score with their log-prob (50-51); one
+    FIXED + KEEP + LOGP step per child adds log p(child | candidate, other parents) from the
+    child's current value (52-78); a SELECT step softmaxes the 8 scores, draws one and
+    broadcasts it to the chain (79-82).  A COLLECT step at the end writes the target (83-87).
+    Every node has its own slots for the whole walk (the sweep reads any node at any time).
+    """
+    model = packed.model
+    order = list(model.topo)
+    kw = dict(latent=latent, fixed=fixed, out_nodes=order, shared_roots=True,
+              exact_f32=exact_f32, kde_valu=kde_valu)
+    init = build_plan(packed, logp=[], mode=MODE_SAMPLE, **kw)
+    full = build_plan(packed, logp=order, mode=MODE_SAMPLE, **kw)       # every row reads its parents
+    assert init.slot_of == full.slot_of
+    rows = full.steps.cpu().numpy()
+    pos = {n: i for i, n in enumerate(order)}
+    lat = [n for n in order if n in set(latent)]
+    children = model.children()
+    table: List[np.ndarray] = []
+    for j, n in enumerate(lat):
+        r = rows[pos[n]].copy()
+        r[S_ROLE] = ROLE_LATENT
+        r[S_FLAGS] |= F_LOGP | F_LPRESET
+        r[S_NOISE] = 2 * j
+        table.append(r)
+        for c in children[n]:
+            r = rows[pos[c]].copy()
+            r[S_ROLE] = ROLE_FIXED
+            r[S_FLAGS] = (r[S_FLAGS] | F_LOGP | F_KEEP) & ~F_SHARED
+            table.append(r)
+        r = rows[pos[n]].copy()
+        r[S_ROLE] = ROLE_SELECT
+        r[S_FLAGS] = 0
+        r[S_NOISE] = 2 * j + 1
+        table.append(r)
+    r = rows[pos[target]].copy()
+    r[S_ROLE] = ROLE_COLLECT
+    r[S_FLAGS] = 0
+    table.append(r)
+    steps = torch.from_numpy(np.ascontiguousarray(np.stack(table))).to(packed.device)
+    return GibbsPlan(init=init, steps=steps, n_steps=len(table), latent=lat, target=target,
+                     n_noise=max(2 * len(lat), 1), in_cols=full.in_cols, kind_mask=full.kind_mask)
