@@ -57,3 +57,31 @@ def test_ris_production_rng_runs_and_normalizes():
     assert w.shape == (2, 512) and xs.shape == (2, 512, 1)
     assert torch.allclose(w.sum(dim=1).cpu(), torch.ones(2), atol=1e-5)
     assert vbn._inference._last_resampled is True
+
+
+def test_gibbs_production_rng_chain_and_reference_modes():
+    """GibbsSampler with Philox draws (gibbs.py:23-92): reference mode repeats the final sweep
+    (gibbs.py:86 collects views), chain mode keeps every collected sweep; both target the same
+    stationary distribution, and evidence on z moves y in the direction of y -> z (weight < 0)."""
+    from vectorizedbayesiannetwork_amd.engines import GibbsSampler
+    vbn = _chain_vbn()
+    B = 1024
+    ev = {"z": torch.cat([torch.full((B // 2, 1), 1.5), torch.full((B // 2, 1), -1.5)])}
+    q = vbn._normalize_query({"target": "y", "evidence": ev})
+    ref = GibbsSampler(n_samples=16, burn_in=20, n_steps=2, seed=3).sample(vbn, q)
+    assert ref.shape == (B, 16, 1) and torch.isfinite(ref).all()
+    assert torch.equal(ref, ref[:, :1].expand_as(ref))
+    chain = GibbsSampler(n_samples=64, burn_in=20, n_steps=2, collect="chain", seed=4).sample(vbn, q)
+    assert chain.shape == (B, 64, 1) and torch.isfinite(chain).all()
+    assert float(chain.std(dim=1).mean()) > 1e-3                          # the chain moves
+    w = float(vbn.model.cpds["z"].state["_weight"].squeeze())
+    for half in (slice(0, B // 2), slice(B // 2, B)):
+        m_ref, m_chain = float(ref[half, 0].mean()), float(chain[half].mean())
+        assert abs(m_ref - m_chain) < 0.15, (m_ref, m_chain)
+    up, down = float(chain[: B // 2].mean()), float(chain[B // 2:].mean())
+    assert (up - down) * w > 0
+    # n_samples = 0 and burn_in = 0: the initial ancestral state (gibbs.py:89-91)
+    x0 = GibbsSampler(n_samples=0, burn_in=0, seed=5).sample(vbn, q, 0)
+    assert x0.shape == (B, 1, 1)
+    with pytest.raises(ValueError, match="collect"):
+        GibbsSampler(collect="bogus")

@@ -541,7 +541,10 @@ def build_gibbs_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Seque
     for j, n in enumerate(lat):
         r = rows[pos[n]].copy()
         r[S_ROLE] = ROLE_LATENT
-        r[S_FLAGS] |= F_LOGP | F_LPRESET
+        # per-chain candidates, roots included: the reference's root candidates are [1, 8, D]
+        # (gibbs.py:50), which it can only index at B = 1 (81); shared root candidates would
+        # correlate every chain of the batch
+        r[S_FLAGS] = (r[S_FLAGS] | F_LOGP | F_LPRESET) & ~F_SHARED
         r[S_NOISE] = 2 * j
         table.append(r)
         for c in children[n]:
