@@ -58,7 +58,9 @@ def main():
     torch.cuda.set_device(0)
     cfg, g, model, vbn, query = Bm.build_workload("cfg2", "cuda:0", 0)
     B = args.chains
-    query = {"target": query["target"], "evidence": {k: v[:B] for k, v in query["evidence"].items()}}
+    reps_ev = -(-B // cfg["B"])                      # more chains than cfg2 queries: tile the evidence rows
+    query = {"target": query["target"],
+             "evidence": {k: v.repeat(reps_ev, 1)[:B].contiguous() for k, v in query["evidence"].items()}}
     vbn.set_sampling_method("gibbs", n_samples=args.n_samples, burn_in=args.burn_in, n_steps=args.thin, seed=1)
     for _ in range(args.warmup):
         vbn.sample(query, n_samples=args.n_samples)
