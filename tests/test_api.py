@@ -126,3 +126,17 @@ def test_engine_accepts_reference_style_vbn_duck_type():
     with pytest.raises(RuntimeError, match="MI355X"):
         MonteCarloMarginalization(n_samples=3).infer_posterior(
             ref, Query(target="b", evidence={"a": torch.zeros(2, 1)}))
+
+
+def test_gibbs_registered_with_yaml_defaults(vbn_cpu):
+    """sampling registry key "gibbs" (gibbs.py:12) with vbn/configs/sampling/gibbs.yaml defaults."""
+    from vectorizedbayesiannetwork_amd.engines import GibbsSampler
+    assert SAMPLING_REGISTRY["gibbs"] is GibbsSampler
+    assert defaults.sampling("gibbs") == {"name": "gibbs", "n_samples": 512, "burn_in": 50, "n_steps": 5}
+    vbn_cpu.set_sampling_method(defaults.sampling("gibbs"))
+    s = vbn_cpu._sampling
+    assert (s.n_samples, s.burn_in, s.n_steps, s.n_candidates) == (512, 50, 5, 8)
+    g = GibbsSampler()                                   # constructor defaults (gibbs.py:14-16)
+    assert (g.n_samples, g.burn_in, g.n_steps) == (200, 10, 1)
+    with pytest.raises(RuntimeError, match="MI355X"):    # no CPU fallback
+        vbn_cpu.sample({"target": "feature_2", "evidence": {"feature_0": torch.zeros(2, 1)}}, n_samples=4)
