@@ -102,3 +102,51 @@ def test_gloo_world2_matches_single_process(hot):
     rpdf, rxs = ref.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}), seed=seed)
     assert torch.equal(pdf, rpdf)
     assert torch.equal(xs, rxs)
+
+
+class StubChainSampler:
+    """Sampler interface of GibbsSampler (``sample(vbn, query, n_samples, seed=...)`` with
+    chains keyed by the global query index ``q_base + b``): a deterministic [b, n, 1] chain."""
+
+    def __init__(self):
+        self.q_base = 0
+
+    def sample(self, vbn, query, n_samples=None, seed=None, **kw):
+        ev = query.evidence["x"]
+        b = ev.shape[0]
+        q = torch.arange(self.q_base, self.q_base + b, dtype=torch.float64).view(b, 1, 1)
+        t = torch.arange(n_samples, dtype=torch.float64).view(1, -1, 1)
+        return (torch.cos(q * 0.9 + t * 0.2 + (seed % 1000) * 1e-3) + ev.view(b, 1, 1)).float()
+
+
+def _chain_worker(rank, world, port, ev, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(123 + rank)
+        eng = ShardedEngine(StubChainSampler(), gather=True)
+        xs = eng.sample(None, Query(target="y", evidence={"x": ev}, do={}), 5)
+        out_q.put((rank, None if xs is None else xs.clone()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_chains_match_single_process():
+    """Gibbs chains shard by query with no data-path collective; the gather rebuilds the batch."""
+    ev = torch.linspace(-1, 1, 5).unsqueeze(1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chain_worker, args=(r, 2, port, ev, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    (_, xs), (_, xs1) = res
+    assert xs1 is None
+    torch.manual_seed(123)
+    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    ref = StubChainSampler().sample(None, Query(target="y", evidence={"x": ev}, do={}), 5, seed=seed)
+    assert torch.equal(xs, ref)
