@@ -830,9 +830,12 @@ def posterior_stats(pdf: torch.Tensor, samples: torch.Tensor, eps: float = 1e-12
 # ----------------------------------------------------------------------------------------
 
 def gibbs(model: BNModel, target: str, evidence: Dict, do: Dict, n_samples: int, draws,
-          burn_in: int = 10, n_steps: int = 1, n_candidates: int = 8) -> torch.Tensor:
+          burn_in: int = 10, n_steps: int = 1, n_candidates: int = 8, copy_collected: bool = False
+          ) -> torch.Tensor:
     """GibbsSampler.sample (gibbs.py:23-92): candidate-reweighting sweeps over the latent
-    nodes, started from one ancestral draw (29); returns ``[b, n_samples, Dt]``."""
+    nodes, started from one ancestral draw (29); returns ``[b, n_samples, Dt]``.
+    ``copy_collected`` keeps each collected sweep's value (the Markov chain, the build's
+    ``collect="chain"``) instead of the reference's views of the final state."""
     b = _batch(evidence, do)
     fixed = _fixed(evidence, do)
     cols, total = _layout(model)
@@ -867,7 +870,8 @@ def gibbs(model: BNModel, target: str, evidence: Dict, do: Dict, n_samples: int,
         if step >= burn_in and (step - burn_in) % thin == 0:             # 83-87
             # a view of ``current`` (no copy): later sweeps overwrite it in place, so every
             # collected entry ends up holding the final sweep's value, as in the reference
-            collected.append(current[..., cols[target]])
+            v = current[..., cols[target]]
+            collected.append(v.clone() if copy_collected else v)
     if not collected:
         return current[..., cols[target]]
     return torch.cat(collected, dim=1)

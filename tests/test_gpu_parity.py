@@ -155,6 +155,12 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
         rxs = O.gibbs(model, q["target"], q["evidence"], q["do"], n, draws, **p)
         _close("samples", xs, rxs, S_ATOL, S_RTOL)
         _close("samples(reference)", xs, case["outputs"]["samples"], S_ATOL, S_RTOL)
+        # chain mode: every collected sweep (oracle keeping copies instead of views)
+        ec = GibbsSampler(n_samples=n, kde_valu=kde_valu, collect="chain", **p)
+        xc = ec.sample(vbn, qq, n, _noise=noise)
+        rxc = O.gibbs(model, q["target"], q["evidence"], q["do"], n, O.ReplayDraws(case["draws"]),
+                      copy_collected=True, **p)
+        _close("samples(chain)", xc, rxc, S_ATOL, S_RTOL)
     else:
         raise AssertionError(eng)
 
