@@ -830,12 +830,15 @@ def posterior_stats(pdf: torch.Tensor, samples: torch.Tensor, eps: float = 1e-12
 # ----------------------------------------------------------------------------------------
 
 def gibbs(model: BNModel, target: str, evidence: Dict, do: Dict, n_samples: int, draws,
-          burn_in: int = 10, n_steps: int = 1, n_candidates: int = 8, copy_collected: bool = False
-          ) -> torch.Tensor:
+          burn_in: int = 10, n_steps: int = 1, n_candidates: int = 8, copy_collected: bool = False,
+          root_expand: bool = False) -> torch.Tensor:
     """GibbsSampler.sample (gibbs.py:23-92): candidate-reweighting sweeps over the latent
     nodes, started from one ancestral draw (29); returns ``[b, n_samples, Dt]``.
     ``copy_collected`` keeps each collected sweep's value (the Markov chain, the build's
-    ``collect="chain"``) instead of the reference's views of the final state."""
+    ``collect="chain"``) instead of the reference's views of the final state.
+    ``root_expand`` broadcasts a latent root's ``[1, 8, D]`` candidates over the b chains: the
+    reference's ``candidates[arange(b), choice]`` (gibbs.py:81) only indexes them at b = 1, so
+    this is the batched CPU timing form (same op sequence), not a parity mode."""
     b = _batch(evidence, do)
     fixed = _fixed(evidence, do)
     cols, total = _layout(model)
@@ -857,6 +860,8 @@ def gibbs(model: BNModel, target: str, evidence: Dict, do: Dict, n_samples: int,
                 pt = pt.expand(b, n_candidates, -1)
             rec = model.cpds[node]
             cand = cpd_sample(rec, pt, n_candidates, draws)              # 50
+            if root_expand and cand.shape[0] != b:
+                cand = cand.expand(b, -1, -1)
             score = cpd_log_prob(rec, cand, pt)                          # 51
             for ch in children[node]:                                    # 52-78
                 cv = current[..., cols[ch]].expand(b, n_candidates, -1)

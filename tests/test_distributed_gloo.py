@@ -150,3 +150,25 @@ def test_gloo_world2_sharded_chains_match_single_process():
     seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
     ref = StubChainSampler().sample(None, Query(target="y", evidence={"x": ev}, do={}), 5, seed=seed)
     assert torch.equal(xs, ref)
+
+
+def test_slice_noise_forms():
+    """Injected draws shard with the queries (ShardedEngine._shard_kwargs): node dicts on axis
+    0, walk tensors [n_latent, 2, B, S, Dmax] on axis 2, Gibbs (init, sweep) pairs with the
+    sweep [iters, n_noise, 2, B, 8, Dmax] on axis 3; broadcast (size-1) batch axes are kept."""
+    from vectorizedbayesiannetwork_amd.distributed import slice_noise
+    B = 5
+    d = {"a": (torch.arange(B * 3.0).view(B, 3), torch.zeros(1, 3)), "b": (None, torch.ones(B, 3, 2))}
+    s = slice_noise(d, 1, 4, B)
+    assert torch.equal(s["a"][0], d["a"][0][1:4]) and s["a"][1].shape == (1, 3)
+    assert s["b"][0] is None and torch.equal(s["b"][1], d["b"][1][1:4])
+    w = torch.randn(2, 2, B, 3, 1)
+    assert torch.equal(slice_noise(w, 2, 5, B), w[:, :, 2:5])
+    sweep = torch.randn(4, 3, 2, B, 8, 1)
+    init, sw = slice_noise((w, sweep), 0, 2, B)
+    assert torch.equal(init, w[:, :, :2]) and torch.equal(sw, sweep[:, :, :, :2])
+    assert slice_noise((None, None), 0, 2, B) == (None, None)
+    with pytest.raises(ValueError):
+        slice_noise(torch.randn(2, 2, B + 1, 3, 1), 0, 2, B)
+    with pytest.raises(ValueError):
+        slice_noise((w, torch.randn(3, B)), 0, 2, B)

@@ -114,14 +114,20 @@ struct Lane {
 
 // Draws of node ``st``, dimension d, for this particle.  Stream 0 gives a standard normal
 // (Box-Muller on both words), stream 1 two uniforms: the categorical / index choice and the
-// within-bin uniform.  Counter = (sample, query ^ seed_hi), key = seed_lo + stream id, where
-// the query key is 0 for draws shared by all queries (root nodes in MCM/LW/ancestral, Q5).
+// within-bin uniform, stream 2 the Gibbs chain choice (one per chain and sweep).  Counter =
+// (sample, query ^ seed_hi), key = seed_lo + stream id, where the query key is 0 for draws
+// shared by all queries (root nodes in MCM/LW/ancestral, Q5).  Stream id = offset[8] |
+// node[14] | dim[8] | stream[2]: disjoint for every (node, dim, stream) the host admits
+// (PackedModel: < 16384 nodes, < 256 dims per node).
 // With injected noise (parity tests) slot 0 = categorical uniform, slot 1 = normal / uniform.
+#define RNG_NORMAL 0
+#define RNG_UNIFORM 1
+#define RNG_SELECT 2
 __device__ __forceinline__ uint2 rng_words(const vbn_walk_args& A, const vbn_step& st, int d, int stream,
                                            const Lane& L) {
   const uint32_t qkey = (st.flags & VBN_F_SHARED) ? 0u : (uint32_t)(A.q_base + L.b + 1);
-  const uint32_t sid = ((uint32_t)(A.offset & 0xffu) << 24) |
-                       (((uint32_t)st.node_id * 16u + (uint32_t)d) * 2u + (uint32_t)stream);
+  const uint32_t sid = ((uint32_t)(A.offset & 0xffu) << 24) | ((uint32_t)st.node_id << 10) |
+                       ((uint32_t)d << 2) | (uint32_t)stream;
   const uint32_t ctr = (uint32_t)L.s + (uint32_t)L.iter * (uint32_t)A.n_samples;
   return philox2x32(make_uint2(ctr, qkey ^ (uint32_t)(A.seed >> 32)), (uint32_t)A.seed + sid);
 }
@@ -137,14 +143,14 @@ __device__ __forceinline__ int64_t noise_index(const vbn_walk_args& A, const vbn
 
 __device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
   if (A.noise) return A.noise[noise_index(A, st, d, 1, L)];
-  const uint2 w = rng_words(A, st, d, 0, L);
+  const uint2 w = rng_words(A, st, d, RNG_NORMAL, L);
   return box_muller(w.x, w.y);
 }
 
 // (categorical uniform, within-bin uniform)
 __device__ __forceinline__ float2 draw_uniforms(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
   if (A.noise) return make_float2(A.noise[noise_index(A, st, d, 0, L)], A.noise[noise_index(A, st, d, 1, L)]);
-  const uint2 w = rng_words(A, st, d, 1, L);
+  const uint2 w = rng_words(A, st, d, RNG_UNIFORM, L);
   return make_float2(u01(w.x), u01(w.y));
 }
 
@@ -1271,12 +1277,11 @@ __device__ __forceinline__ void gibbs_select(const vbn_walk_args& A, const vbn_s
   float pk[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) pk[k] = __shfl(e, g0 + k) / se;
-  // one uniform per chain (candidate lane 0's draw), multinomial(weights, 1) (80)
-  // (without injected noise the draw uses dimension stream 15 of the node, which no candidate
-  // draw of a node with fewer than 16 dims touches)
+  // one uniform per chain (candidate lane 0's draw), multinomial(weights, 1) (80); without
+  // injected noise it comes from the node's own SELECT stream, which no candidate draw uses
   const int s_keep = L.s;
   L.s = 0;
-  const float u = A.noise ? draw_uniforms(A, st, 0, L).x : u01(rng_words(A, st, 15, 1, L).x);
+  const float u = A.noise ? draw_uniforms(A, st, 0, L).x : u01(rng_words(A, st, 0, RNG_SELECT, L).x);
   L.s = s_keep;
   const int idx = inv_cdf(8, u, [&](int k) { return pk[k]; });
   for (int d = 0; d < st.out_dim; ++d) {

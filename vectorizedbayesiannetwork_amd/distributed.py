@@ -38,6 +38,39 @@ def shard_query(query, b0: int, b1: int) -> Query:
     return Query(target=query.target, evidence=ev, do=do)
 
 
+def _slice_rows(t, axis: int, b0: int, b1: int, n_total: int):
+    """Rows [b0, b1) of a per-query tensor along ``axis``; a broadcast (size-1) axis is kept."""
+    if t is None or not isinstance(t, torch.Tensor):
+        return t
+    if t.dim() <= axis or t.shape[axis] == 1:
+        return t
+    if t.shape[axis] != n_total:
+        raise ValueError(f"injected noise has {t.shape[axis]} rows on axis {axis}, expected {n_total} or 1")
+    return t.narrow(axis, b0, b1 - b0)
+
+
+def slice_noise(noise, b0: int, b1: int, n_total: int):
+    """Shard injected draws (``_noise`` / ``_noise_fallback``) with the queries.
+
+    Forms (engines.noise_tensor, GibbsSampler.sample): a dict node -> (slot0, slot1) of
+    [B|1, S(, D)] tensors (batch axis 0); a walk tensor [n_latent, 2, B|1, S, Dmax] (axis 2);
+    a Gibbs pair (init, sweep) with init in either walk form and sweep
+    [iters, n_noise, 2, B, 8, Dmax] (axis 3).
+    """
+    if noise is None:
+        return None
+    if isinstance(noise, dict):
+        return {k: tuple(_slice_rows(v, 0, b0, b1, n_total) for v in vs) for k, vs in noise.items()}
+    if isinstance(noise, (tuple, list)) and len(noise) == 2:          # Gibbs (init, sweep)
+        init, sweep = noise
+        if sweep is not None and (not isinstance(sweep, torch.Tensor) or sweep.dim() != 6):
+            raise ValueError("Gibbs sweep noise must be [iters, n_noise, 2, B, 8, Dmax]")
+        return (slice_noise(init, b0, b1, n_total), _slice_rows(sweep, 3, b0, b1, n_total))
+    if isinstance(noise, torch.Tensor) and noise.dim() == 5:
+        return _slice_rows(noise, 2, b0, b1, n_total)
+    raise ValueError("unrecognised injected-noise form for a sharded call")
+
+
 def _world(group) -> Tuple[int, int]:
     if not dist.is_available() or not dist.is_initialized():
         return 0, 1
@@ -104,6 +137,16 @@ class ShardedEngine:
                for r in range(world)]
         return torch.cat(out, dim=0)
 
+    def _shard_kwargs(self, kwargs, b0: int, b1: int, n_total: int) -> dict:
+        kw = dict(kwargs)
+        kw["seed"] = self._shared_seed(kwargs)
+        for k in ("_noise", "_noise_fallback"):
+            if k in kw:
+                kw[k] = slice_noise(kw[k], b0, b1, n_total)
+        if kw.get("_resample_u"):                    # RIS resampling uniforms, [B, S] each
+            kw["_resample_u"] = [_slice_rows(u, 0, b0, b1, n_total) for u in kw["_resample_u"]]
+        return kw
+
     def _check(self, n_total: int, world: int) -> None:
         if n_total < world:
             raise ValueError(f"{n_total} queries cannot be sharded over {world} ranks")
@@ -114,8 +157,7 @@ class ShardedEngine:
         self._check(n_total, world)
         b0, b1 = shard_bounds(n_total, rank, world)
         self._set_base(b0)
-        kw = dict(kwargs)
-        kw["seed"] = self._shared_seed(kwargs)
+        kw = self._shard_kwargs(kwargs, b0, b1, n_total)
         red = self._flag_reducer()
         if red is not None:
             kw["_reduce_flag"] = red
@@ -130,8 +172,7 @@ class ShardedEngine:
         self._check(n_total, world)
         b0, b1 = shard_bounds(n_total, rank, world)
         self._set_base(b0)
-        kw = dict(kwargs)
-        kw["seed"] = self._shared_seed(kwargs)
+        kw = self._shard_kwargs(kwargs, b0, b1, n_total)
         xs = self.engine.sample(vbn, shard_query(query, b0, b1), n_samples, **kw)
         if not self.gather or isinstance(xs, dict):
             return xs

@@ -521,7 +521,11 @@ class ResampledImportanceSampling(_EngineBase):
                     break
                 w, ess = ops.normalize_weights(st_a[plan.n_slots].view(b, n), True, 0.0)     # 85-87
                 self._last_ess = ess
-                if bool((ess < threshold).any()):                                            # 88-90
+                flag = (ess < threshold).any()
+                reduce = kwargs.get("_reduce_flag")          # multi-GPU: batch-global decision
+                if reduce is not None:
+                    flag = reduce(flag)
+                if bool(flag):                                                               # 88-90
                     u = u_list.pop(0) if u_list else None
                     ops.resample(w, u, seed, events + 1, self.q_base, st_a, st_b)
                     st_a, st_b = st_b, st_a
@@ -607,7 +611,13 @@ class GibbsSampler(_EngineBase):
         if target not in model.cpds:
             raise ValueError(f"Unknown target node: {target}")
         vals = _fixed_values(query, dev)
-        _check_discrete(pk, vals, list(ev))
+        thin = max(self.n_steps, 1)
+        iters = self.burn_in + n * thin                                                 # 37
+        if iters > 0:
+            # every sweep scores the observed children of latent nodes, evidence and do nodes
+            # alike (gibbs.py:56-78), so out-of-class values raise as in softmax_nn._x_to_bin
+            _check_discrete(pk, vals, [x for x in model.topo if x in vals
+                                       and any(p not in vals for p in model.parents[x])])
         gp = self._gibbs_plan(pk, target, vals)
         init = gp.init
         fx = _fixed_buffer(init, vals, b, dev)
@@ -616,8 +626,6 @@ class GibbsSampler(_EngineBase):
         state = torch.empty(init.n_slots + 1, b, device=dev, dtype=torch.float32)
         _, x0 = run_walk(pk, init, fx, b, 1, seed=seed, q_base=self.q_base, noise=init_noise,
                          state=state, state_flags=2)                                    # gibbs.py:29
-        thin = max(self.n_steps, 1)
-        iters = self.burn_in + n * thin                                                 # 34
         slot, dt = init.slot_of[target], model.out_dim(target)
         if iters == 0:
             return x0[..., slot:slot + dt].contiguous()                                 # 89-91

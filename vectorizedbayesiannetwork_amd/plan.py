@@ -41,6 +41,8 @@ STEP_INTS = 32
 KDE_CHUNKS = 16
 MLP_HIDDEN = (32, 32)
 KDE_MAX_DIMS = 4
+MAX_NODES = 1 << 14
+MAX_NODE_DIMS = 1 << 8
 
 
 def _row(r: int, h: int) -> int:
@@ -308,7 +310,12 @@ class PackedModel:
         blob = _Blob()
         blob.add(np.zeros(4, np.float32))                 # offset 0 is never a real block
         self.nodes: Dict[str, NodePack] = {}
+        # Philox stream ids pack (node, dim, stream) into 14 + 8 + 2 bits (csrc rng_words)
+        if len(model.topo) >= MAX_NODES:
+            raise NotImplementedError(f"{len(model.topo)} nodes: the walk keys RNG streams for < {MAX_NODES}")
         for node in model.topo:
+            if model.out_dim(node) >= MAX_NODE_DIMS:
+                raise NotImplementedError(f"node {node}: {model.out_dim(node)} dims (max {MAX_NODE_DIMS - 1})")
             rec = model.cpds[node]
             expect = sum(model.out_dim(p) for p in model.parents[node])
             if rec.input_dim != expect:
