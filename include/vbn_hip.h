@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 4
+#define VBN_ABI_VERSION 5
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001
@@ -101,7 +101,11 @@ enum vbn_mode {
                              n_samples = 8 candidates; out_x = [B][n_collect][n_out_cols]    */
 };
 
-/* One node of the topological walk (32 x int32, filled by the host plan packer). */
+/* One node of the topological walk (32 x int32, filled by the host plan packer).
+ * reserved[0] = split-f16 W2 fragments; [1..4] = KDE point packs; [5] = wblk_off, [6] =
+ * wblk_len: the NN CPD's weight block [W1 fragments | accumulator-init biases | split-f16 W2]
+ * (params float offset, length in floats, a multiple of 256), which the walk stages into LDS
+ * one step ahead (0 = the step runs no MLP). */
 typedef struct vbn_step {
   int32_t kind, role, flags, act;
   int32_t n_in, in_off, out_col, out_dim;
@@ -145,6 +149,8 @@ typedef struct vbn_walk_args {
   int32_t gibbs_burn_in;
   int32_t gibbs_thin;
   int32_t n_noise;         /* noise nodes per sweep (injected-noise stride, mode GIBBS) */
+  int32_t wbuf_floats;     /* >= every step's wblk_len: size of each of the two LDS weight
+                              buffers shared by the waves of a workgroup                */
 } vbn_walk_args;
 
 int vbn_hip_abi_version(void);
@@ -192,7 +198,8 @@ int vbn_hip_rb_epilogue(const float* log_w, const float* params, int64_t params_
                         float* pdf, float* grid, int64_t n_queries, int32_t n_particles, int32_t n_out,
                         int32_t mode, float stddevs, float min_scale, float eps, void* stream);
 
-/* LDS bytes one 64-particle wave needs for a plan (host helper). */
+/* LDS bytes of one 64-particle wave's value slots + head scratch (host helper); a workgroup
+ * of w waves also holds two weight buffers of wbuf_floats each. */
 int64_t vbn_hip_lds_bytes(int32_t n_slots, int32_t max_out);
 
 #ifdef __cplusplus

@@ -100,15 +100,19 @@ def emulate_mlp(P, row, parents64, std, split=False):
             for s in range(16):
                 b = mfma_32x32x2(w2[s // 4, :, s % 4], hb[:, s], b)
         h2.append(b)
-    X = np.zeros((64, 16)); Y = np.zeros((64, 16))
-    for r in range(16):
-        x, y = permlane32_swap(h2[0][:, r], h2[1][:, r])
-        X[:, r] = np.maximum(x, 0)
-        Y[:, r] = np.maximum(y, 0)
+    # head in the accumulator layout (csrc mlp_head): lane half h sums its 16 rows with the
+    # weights w3[j][16 h + r], one permlane32 swap per output adds the halves
     n_out = row[10]
     w3 = P[row[S_OFF_W3]: row[S_OFF_W3] + 32 * n_out].reshape(n_out, 32)
     b3 = P[row[S_OFF_B3]: row[S_OFF_B3] + n_out]
-    return (X @ w3[:, :16].T + Y @ w3[:, 16:].T + b3).T
+    out = np.zeros((n_out, 64))
+    for j in range(n_out):
+        wl = w3[j].reshape(2, 16)[half]                              # [64, 16]
+        p0 = (wl * np.maximum(h2[0], 0)).sum(1)
+        p1 = (wl * np.maximum(h2[1], 0)).sum(1)
+        a, b = permlane32_swap(p0, p1)
+        out[j] = a + b + b3[j]
+    return out
 
 
 @pytest.mark.parametrize("name", ["readme", "family_gaussian_nn", "family_mdn", "mix12"])
@@ -143,6 +147,44 @@ def test_mfma_fragment_packing_reproduces_torch_mlp(name):
         np.testing.assert_allclose(got_split, h.numpy().T, rtol=2e-5, atol=2e-5)
         checked += 1
     assert checked > 0
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg5"])
+def test_weight_blocks_cover_the_mlp_fragments(cfg):
+    """Each NN step's LDS-staged weight block (wblk_off, wblk_len) starts at W1 and holds the
+    accumulator-init biases, the split-f16 W2 fragments and the head; lengths are whole 1-KiB
+    DMA chunks; plan.wbuf is the largest block; steps without an MLP stage nothing."""
+    from vectorizedbayesiannetwork_amd.plan import (S_KIND, S_NOUT, S_WBLK_LEN, S_WBLK_OFF, WBLK_CHUNK, F_ROOT,
+                                                    build_gibbs_plan, ROLE_SELECT, ROLE_COLLECT)
+    c = synthetic.CONFIGS[cfg]
+    g = synthetic.random_dag(c["n_nodes"], seed=0)
+    model = random_init_model(g, synthetic.round_robin_kinds(g, c["kinds"]), synthetic.sem_data(g, 300, seed=0),
+                              overrides={"kde": {"max_points": 64}})
+    pk = PackedModel(model, torch.device("cpu"))
+    target, ev = synthetic.default_query_nodes(g, seed=1)
+    latent = [n for n in model.topo if n not in ev]
+    plan = build_plan(pk, latent=latent, fixed=ev, logp=[target] + ev, out_nodes=[target],
+                      shared_roots=True, mode=MODE_MCM)
+    steps = plan.steps.numpy()
+    nn = 0
+    for row in steps:
+        mlp = row[S_KIND] in (0, 2, 4) and not (row[S_FLAGS] & F_ROOT) and (
+            row[S_ROLE] == ROLE_LATENT or (row[S_FLAGS] & F_LOGP))
+        if not mlp:
+            assert row[S_WBLK_LEN] == 0
+            continue
+        nn += 1
+        off, ln = row[S_WBLK_OFF], row[S_WBLK_LEN]
+        assert off == row[S_OFF_W1] and ln > 0 and ln % WBLK_CHUNK == 0
+        assert off % 4 == 0 and row[S_OFF_B2] % 4 == 0 and row[S_OFF_W2H] % 4 == 0 and row[S_OFF_W3] % 4 == 0
+        assert off < row[S_OFF_B2] < row[S_OFF_W2H] < row[S_OFF_W3] <= row[S_OFF_B3]
+        assert row[S_OFF_B2] + 128 <= row[S_OFF_W2H] and row[S_OFF_W2H] + 1024 <= row[S_OFF_W3]
+        assert row[S_OFF_B3] + row[S_NOUT] <= off + ln <= pk.params.numel()
+    assert nn > 0 and plan.wbuf == steps[:, S_WBLK_LEN].max()
+    gp = build_gibbs_plan(pk, latent=latent, fixed=ev, target=target)
+    gs = gp.steps.numpy()
+    sel = (gs[:, S_ROLE] == ROLE_SELECT) | (gs[:, S_ROLE] == ROLE_COLLECT)
+    assert (gs[sel, S_WBLK_LEN] == 0).all() and gp.wbuf == gs[:, S_WBLK_LEN].max() > 0
 
 
 def _check_liveness(model, plan):

@@ -27,6 +27,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "vbn_hip.h"
 
 #define WAVE 64
@@ -71,6 +73,9 @@ __device__ __forceinline__ float act_fn(float x) {
 // log1p(e) as Kahan's log(u) * e / (u - 1) (u - 1 is exact) for x >= -5, a 4-term series
 // below (relative error < 1e-9 there).
 __device__ __forceinline__ float softplus_t(float x) {
+#ifdef VBN_ABL_NOSOFTPLUS
+  return x;
+#endif
   if (x > 20.f) return x;
   const float e = __expf(x);
   if (x < -5.f) return e * (1.f - e * (0.5f - e * (0.33333334f - e * 0.25f)));
@@ -104,6 +109,7 @@ struct Lane {
   const int32_t* ic;     // parent column slots (from a __restrict__ kernel argument)
   float* vals;   // LDS [n_slots][64]
   float* scr;    // LDS [max_out][64]
+  const float* wb;  // LDS: this step's weight block (wblk, staged one step ahead by the workgroup)
   int lane;
   int64_t p;     // particle (clamped)
   int64_t b;     // query (Gibbs: chain)
@@ -143,6 +149,9 @@ __device__ __forceinline__ int64_t noise_index(const vbn_walk_args& A, const vbn
 
 __device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
   if (A.noise) return A.noise[noise_index(A, st, d, 1, L)];
+#ifdef VBN_ABL_NORNG
+  return 0.5f;
+#endif
   const uint2 w = rng_words(A, st, d, RNG_NORMAL, L);
   return box_muller(w.x, w.y);
 }
@@ -219,34 +228,23 @@ __device__ __forceinline__ float l1_operand(const vbn_walk_args& A, const vbn_st
   return kk < nin ? z : 0.0f;
 }
 
-// layer-1 accumulator of group g: b1 + W1 z (K = n_in, k-steps of 2)
-template <bool STD, int NIN>
-__device__ __forceinline__ f32x16 mlp_layer1(const vbn_walk_args& A, const vbn_step& st, const Lane& L, int g) {
-  const float* __restrict__ P = L.P;
-  const int lane = L.lane;
-  const float4* bacc = reinterpret_cast<const float4*>(P + st.off_b2 + 32 * g + 16 * (lane >> 5));
+#define WBLK_OFF(st) ((st).reserved[5])
+#define WBLK_LEN(st) ((st).reserved[6])
+
+// Layer-1 accumulator init of group g = bias rows of the lane half (register r of half h =
+// b1[row(r, h)]), from the staged weight block (LDS) or, on the exact fallback, the blob.
+__device__ __forceinline__ f32x16 load_acc16(const float* __restrict__ src) {
+  const float4* q4 = reinterpret_cast<const float4*>(src);
   f32x16 a;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const float4 v = bacc[q];
+    const float4 v = q4[q];
     a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-  }
-  if (NIN > 0) {
-#pragma unroll
-    for (int t = 0; t < (NIN + 1) / 2; ++t)
-      a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
-                                               l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
-  } else {
-    const int t1 = (st.n_in + 1) >> 1;
-    for (int t = 0; t < t1; ++t)
-      a = __builtin_amdgcn_mfma_f32_32x32x2f32(P[st.off_w1 + t * WAVE + lane],
-                                               l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
   }
   return a;
 }
 
-// layer-2 bias as the accumulator's initial value (one copy per group: distinct addresses keep
-// the two groups' loads apart, so each lands directly in its accumulator)
+// layer-2 bias as the accumulator's initial value of group g (exact f32 fallback path)
 __device__ __forceinline__ f32x16 layer2_init(const vbn_step& st, const Lane& L, int g) {
   const float4* bacc = reinterpret_cast<const float4*>(L.P + st.off_b2 + 64 + 32 * g + 16 * (L.lane >> 5));
   f32x16 b;
@@ -271,20 +269,16 @@ __device__ __forceinline__ float sub_f16_hi(float y, uint32_t hp) {
   return r;
 }
 
-// Layer 2 of one group on the split-f16 path: y = act(a); y = hi + lo with hi = f16(y),
-// lo = f16(y - hi); A_lo.B_hi + A_hi.B_lo + A_hi.B_hi on v_mfma_f32_32x32x16_f16 (f32
-// accumulate).  B operand: register 8s+j of lane half h holds hidden row 16s + 8(j>>2) +
-// 4h + (j&3).  Returns false (wave-uniform) when some |y| > 32768 (outside the f16 split range).
-template <int ACT>
-__device__ __forceinline__ bool layer2_split(const vbn_step& st, const Lane& L, int g, const f32x16& a, f32x16& out) {
-  float y[16];
-  int big = 0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    y[r] = act_fn<ACT>(a[r]);
-    big = max(big, __float_as_int(y[r]));        // activations are >= -1: only the positive side
-  }
-  if (__any(big > 0x47000000)) return false;     // (NaN with the sign bit clear counts as big)
+// Layer 2 of one group on the split-f16 path from the activations y (|y| <= 32768 checked by
+// the caller): y = hi + lo with hi = f16(y), lo = f16(y - hi); A_lo.B_hi + A_hi.B_lo + A_hi.B_hi
+// on v_mfma_f32_32x32x16_f16 (f32 accumulate).  B operand: register 8s+j of lane half h holds
+// hidden row 16s + 8(j>>2) + 4h + (j&3).
+__device__ __forceinline__ f32x16 layer2_split(const uint4 (&w2h)[4], const f32x16& binit, const float (&y)[16]) {
+#ifdef VBN_ABL_NOL2
+  f32x16 r = binit;
+  for (int i = 0; i < 16; ++i) r[i] += y[i];
+  return r;
+#endif
   f16x8 bh[2], bl[2];
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
@@ -293,115 +287,206 @@ __device__ __forceinline__ bool layer2_split(const vbn_step& st, const Lane& L, 
       const float y0 = y[8 * s2 + j], y1 = y[8 * s2 + j + 1];
       const f16x2 ph = __builtin_convertvector((f32x2){y0, y1}, f16x2);
       const uint32_t hp = __builtin_bit_cast(uint32_t, ph);
+#ifdef VBN_ABL_NOSPLIT
+      const f16x2 pl = ph;
+#else
       const f16x2 pl = __builtin_convertvector((f32x2){sub_f16_lo(y0, hp), sub_f16_hi(y1, hp)}, f16x2);
+#endif
       bh[s2][j] = ph[0];
       bh[s2][j + 1] = ph[1];
       bl[s2][j] = pl[0];
       bl[s2][j + 1] = pl[1];
     }
   }
-  const uint4* w2h = reinterpret_cast<const uint4*>(L.P + OFF_W2H(st));
-  f32x16 b = layer2_init(st, L, g);
+  f32x16 b = binit;
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2) {
-    const f16x8 ah = __builtin_bit_cast(f16x8, w2h[s2 * WAVE + L.lane]);
-    const f16x8 al = __builtin_bit_cast(f16x8, w2h[(2 + s2) * WAVE + L.lane]);
+    const f16x8 ah = __builtin_bit_cast(f16x8, w2h[s2]);
+    const f16x8 al = __builtin_bit_cast(f16x8, w2h[2 + s2]);
+#ifndef VBN_ABL_NOSPLIT
     b = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s2], b, 0, 0, 0);
     b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s2], b, 0, 0, 0);
+#endif
     b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s2], b, 0, 0, 0);
   }
-  out = b;
-  return true;
+  return b;
 }
 
-// Layer 2 of one group, exact f32 chain (K = 32 as 16 v_mfma_f32_32x32x2_f32 steps)
-template <int ACT>
-__device__ __forceinline__ f32x16 layer2_exact(const vbn_step& st, const Lane& L, int g, const f32x16& a) {
+// Layer 2 of one group from the activations y, exact f32 chain (K = 32 as 16
+// v_mfma_f32_32x32x2_f32 steps)
+__device__ __forceinline__ f32x16 layer2_exact(const vbn_step& st, const Lane& L, int g, const float (&y)[16]) {
   const float4* w2p = reinterpret_cast<const float4*>(L.P + st.off_w2);
   f32x16 b = layer2_init(st, L, g);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const float4 v = w2p[q * WAVE + L.lane];
-    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, act_fn<ACT>(a[4 * q + 0]), b, 0, 0, 0);
-    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, act_fn<ACT>(a[4 * q + 1]), b, 0, 0, 0);
-    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, act_fn<ACT>(a[4 * q + 2]), b, 0, 0, 0);
-    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, act_fn<ACT>(a[4 * q + 3]), b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, y[4 * q + 0], b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, y[4 * q + 1], b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, y[4 * q + 2], b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, y[4 * q + 3], b, 0, 0, 0);
   }
   return b;
 }
 
-// transpose (lane l <- all 32 hidden units of particle l), activation, head on VALU with
-// wave-uniform weight pairs (v_pk_fma_f32), outputs to scr[j][lane]
+// Head on VALU in the accumulator layout (no transpose): lane half h holds hidden rows
+// row(r, h) of its particle, so per output j the half's 16 products use per-lane weights
+// W3[j][row(r, h)] (the pack's [n_out][32] rows hold 16 per half), in two independent chains
+// per group; one v_permlane32_swap per output then adds the two halves (group 0 | group 1 ->
+// lane l = particle l).  W = the step's weight block (W3 at off_w3, b3 at off_b3, relative to
+// wblk_off); outputs to scr[j][lane].
 template <int ACT>
-__device__ __forceinline__ void mlp_head(const vbn_step& st, const Lane& L, const f32x16& h0, const f32x16& h1,
-                                         bool nan_in) {
-  const float* __restrict__ P = L.P;
-  f32x2 X[8], Y[8];
+__device__ __forceinline__ void mlp_head(const vbn_step& st, const Lane& L, const float* __restrict__ W,
+                                         const f32x16& h0, const f32x16& h1, bool nan_in) {
+  const int lane = L.lane;
+#ifdef VBN_ABL_NOHEAD
+  for (int j = 0; j < st.n_out; ++j) L.scr[j * WAVE + lane] = h0[j] + h1[j + 1];
+  wave_sync();
+  return;
+#endif
+  float y0[16], y1[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(h0[r]), __float_as_uint(h1[r]), false, false);
-    X[r >> 1][r & 1] = act_fn<ACT>(__uint_as_float(sw[0]));   // hidden row(r, 0)
-    Y[r >> 1][r & 1] = act_fn<ACT>(__uint_as_float(sw[1]));   // hidden row(r, 1)
+    y0[r] = act_fn<ACT>(h0[r]);
+    y1[r] = act_fn<ACT>(h1[r]);
   }
   const int nout = st.n_out;
-  const f32x2* __restrict__ w3 = reinterpret_cast<const f32x2*>(P + st.off_w3);
-#pragma clang loop vectorize(disable) interleave(disable) unroll(disable)
+  const float* __restrict__ w3 = W + (st.off_w3 - WBLK_OFF(st)) + 16 * (lane >> 5);
+  const float* __restrict__ b3 = W + (st.off_b3 - WBLK_OFF(st));
+#pragma clang loop unroll(disable)
   for (int j = 0; j < nout; ++j) {
-    f32x2 o = {P[st.off_b3 + j], 0.f};
+    const float4* w4 = reinterpret_cast<const float4*>(w3 + 32 * j);
+    float wv[16];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o = __builtin_elementwise_fma(w3[j * 16 + i], X[i], o);
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = w4[q];
+      wv[4 * q] = v.x; wv[4 * q + 1] = v.y; wv[4 * q + 2] = v.z; wv[4 * q + 3] = v.w;
+    }
+    float a0 = 0.f, c0 = 0.f, a1 = 0.f, c1 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o = __builtin_elementwise_fma(w3[j * 16 + 8 + i], Y[i], o);
-    L.scr[j * WAVE + L.lane] = nan_in ? __int_as_float(0x7fc00000) : o[0] + o[1];
+    for (int r = 0; r < 16; r += 2) {
+      a0 = fmaf(wv[r], y0[r], a0);
+      c0 = fmaf(wv[r + 1], y0[r + 1], c0);
+      a1 = fmaf(wv[r], y1[r], a1);
+      c1 = fmaf(wv[r + 1], y1[r + 1], c1);
+    }
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0 + c0), __float_as_uint(a1 + c1), false, false);
+    const float o = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + b3[j];
+    L.scr[j * WAVE + lane] = nan_in ? __int_as_float(0x7fc00000) : o;
   }
   wave_sync();
 }
 
-template <int ACT, bool STD, int NIN>
-__device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+// Layer 1 of group g (v_mfma_f32_32x32x2_f32, K = n_in, bias rows as the accumulator init)
+// and its activation.  W = weight block base (LDS: staged block; global: blob + wblk_off), so
+// W1 sits at W[t * 64 + lane] and the biases at W + (off_b2 - wblk_off).  ``pre`` runs between
+// the fragment reads and the first MFMA (group 0: the step's draws).  Returns true
+// (wave-uniform) when some activation leaves the f16 split range |y| <= 32768 (NaN with the
+// sign bit clear counts as out of range).
+template <int ACT, bool STD, int NIN, typename F>
+__device__ __forceinline__ bool mlp_l1_act(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
+                                           const float* __restrict__ W, int g, float (&y)[16], F&& pre) {
+  const int lane = L.lane;
+  f32x16 a = load_acc16(W + (st.off_b2 - WBLK_OFF(st)) + 32 * g + 16 * (lane >> 5));
+  if (NIN > 0) {
+    float w1[(NIN + 1) / 2 > 0 ? (NIN + 1) / 2 : 1];
+#pragma unroll
+    for (int t = 0; t < (NIN + 1) / 2; ++t) w1[t] = W[t * WAVE + lane];
+    pre();
+#pragma unroll
+    for (int t = 0; t < (NIN + 1) / 2; ++t)
+      a = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[t], l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
+  } else {
+    pre();
+    const int t1 = (st.n_in + 1) >> 1;
+    for (int t = 0; t < t1; ++t)
+      a = __builtin_amdgcn_mfma_f32_32x32x2f32(W[t * WAVE + lane], l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
+  }
+  int big = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    y[r] = act_fn<ACT>(a[r]);
+    big = max(big, __float_as_int(y[r]));        // activations are >= -1: only the positive side
+  }
+  return __any(big > 0x47000000);
+}
+
+// One NN node for the wave's 64 particles from the LDS-staged weight block: group 0 (layer 1,
+// range check, layer 2 split-f16 on MFMA), then group 1, the head on both.  ``pre`` (the
+// step's draws, independent of the MLP) runs after group 0's fragment reads are issued.  An
+// f16-range miss in either group, or VBN_F_F32L2, sends both groups to the exact f32 chain
+// (layer 1 recomputed there from the blob).
+template <int ACT, bool STD, int NIN, typename F>
+__device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
+  const int lane = L.lane;
   const int nin = NIN > 0 ? NIN : st.n_in;
+  const float* __restrict__ W = L.wb;
+  const uint4* w2h = reinterpret_cast<const uint4*>(W + (OFF_W2H(st) - WBLK_OFF(st)));
+  const float* b2 = W + (st.off_b2 - WBLK_OFF(st)) + 64 + 16 * (lane >> 5);
   bool nan_in = false;                            // torch keeps NaN through Linear/act
   for (int d = 0; d < nin; ++d) {
-    const float v = L.vals[L.ic[st.in_off + d] * WAVE + L.lane];
+    const float v = L.vals[L.ic[st.in_off + d] * WAVE + lane];
     nan_in |= (v != v);
   }
-  // split path unless flagged off or some |hidden| leaves the f16 range (wave-uniform); one
-  // shared head after the merge (an early-return shape doubles the live registers)
   f32x16 h0, h1;
-  if ((st.flags & VBN_F_F32L2) || !(layer2_split<ACT>(st, L, 0, mlp_layer1<STD, NIN>(A, st, L, 0), h0) &&
-                                    layer2_split<ACT>(st, L, 1, mlp_layer1<STD, NIN>(A, st, L, 1), h1))) {
-    h0 = layer2_exact<ACT>(st, L, 0, mlp_layer1<STD, NIN>(A, st, L, 0));
-    h1 = layer2_exact<ACT>(st, L, 1, mlp_layer1<STD, NIN>(A, st, L, 1));
+  bool exact = (st.flags & VBN_F_F32L2) != 0;
+  bool pre_done = false;
+  if (!exact) {
+    float y[16];
+    pre_done = true;
+    if (mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 0, y, pre)) {
+      exact = true;
+    } else {
+      const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
+      h0 = layer2_split(wq, load_acc16(b2), y);
+    }
   }
-  mlp_head<ACT>(st, L, h0, h1, nan_in);
+  if (!exact) {
+    float y[16];
+    if (mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 1, y, [] {})) {
+      exact = true;
+    } else {
+      const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
+      h1 = layer2_split(wq, load_acc16(b2 + 32), y);
+    }
+  }
+  if (exact) {
+    if (!pre_done) pre();
+    const float* __restrict__ Wg = L.P + WBLK_OFF(st);
+    float y[16];
+    mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 0, y, [] {});
+    h0 = layer2_exact(st, L, 0, y);
+    mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 1, y, [] {});
+    h1 = layer2_exact(st, L, 1, y);
+  }
+  mlp_head<ACT>(st, L, W, h0, h1, nan_in);
 }
 
-template <int ACT, bool STD>
-__device__ __forceinline__ void mlp_nin(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+template <int ACT, bool STD, typename F>
+__device__ __forceinline__ void mlp_nin(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
   switch (st.n_in) {
-    case 1: mlp_forward<ACT, STD, 1>(A, st, L); break;
-    case 2: mlp_forward<ACT, STD, 2>(A, st, L); break;
-    case 3: mlp_forward<ACT, STD, 3>(A, st, L); break;
-    default: mlp_forward<ACT, STD, 0>(A, st, L); break;
+    case 1: mlp_forward<ACT, STD, 1>(A, st, L, pre); break;
+    case 2: mlp_forward<ACT, STD, 2>(A, st, L, pre); break;
+    case 3: mlp_forward<ACT, STD, 3>(A, st, L, pre); break;
+    default: mlp_forward<ACT, STD, 0>(A, st, L, pre); break;
   }
 }
 
-// KM bit 5: some NN CPD uses a non-relu activation
-template <unsigned KM>
-__device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+// KM bit 5: some NN CPD uses a non-relu activation.  ``pre``: the step's draws (see mlp_forward).
+template <unsigned KM, typename F>
+__device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
   const bool sd = (st.flags & VBN_F_STANDARDIZE) != 0;
   if (!(KM & 32) || st.act == VBN_ACT_RELU) {
-    if (sd) mlp_nin<VBN_ACT_RELU, true>(A, st, L); else mlp_nin<VBN_ACT_RELU, false>(A, st, L);
+    if (sd) mlp_nin<VBN_ACT_RELU, true>(A, st, L, pre); else mlp_nin<VBN_ACT_RELU, false>(A, st, L, pre);
     return;
   }
   if constexpr ((KM & 32) != 0) {
     switch (st.act * 2 + (sd ? 1 : 0)) {
-      case 2: mlp_nin<VBN_ACT_TANH, false>(A, st, L); break;
-      case 3: mlp_nin<VBN_ACT_TANH, true>(A, st, L); break;
-      case 4: mlp_nin<VBN_ACT_GELU, false>(A, st, L); break;
-      case 5: mlp_nin<VBN_ACT_GELU, true>(A, st, L); break;
-      case 6: mlp_nin<VBN_ACT_ELU, false>(A, st, L); break;
-      default: mlp_nin<VBN_ACT_ELU, true>(A, st, L); break;
+      case 2: mlp_nin<VBN_ACT_TANH, false>(A, st, L, pre); break;
+      case 3: mlp_nin<VBN_ACT_TANH, true>(A, st, L, pre); break;
+      case 4: mlp_nin<VBN_ACT_GELU, false>(A, st, L, pre); break;
+      case 5: mlp_nin<VBN_ACT_GELU, true>(A, st, L, pre); break;
+      case 6: mlp_nin<VBN_ACT_ELU, false>(A, st, L, pre); break;
+      default: mlp_nin<VBN_ACT_ELU, true>(A, st, L, pre); break;
     }
   }
 }
@@ -445,7 +530,13 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
     }
     return;
   }
-  run_mlp<KM>(A, st, L);
+  float eps0 = 0.f;                                 // dim-0 draw, issued beside the weight loads
+#ifdef VBN_LATE_DRAW
+  run_mlp<KM>(A, st, L, [] {});
+  if (latent) eps0 = draw_normal(A, st, 0, L);
+#else
+  run_mlp<KM>(A, st, L, [&]() { if (latent) eps0 = draw_normal(A, st, 0, L); });
+#endif
   const float min_scale = t[2 * D];
   float acc = 0.f;
   for (int d = 0; d < D; ++d) {
@@ -461,7 +552,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
     }
     float x;
     if (latent) {
-      x = loc + draw_normal(A, st, d, L) * scale;
+      x = loc + (d == 0 ? eps0 : draw_normal(A, st, d, L)) * scale;
     } else {
       x = node_fixed(A, st, d, L);
     }
@@ -547,8 +638,16 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
   const int lane = L.lane;
   float* scr = L.scr;
   float min_scale = 0.f, lmax = 0.f, lsum = 1.f, psum = 1.f;
+  float u0 = 0.f, eps0 = 0.f;                       // component choice + dim-0 normal
+  auto draws = [&]() {
+    if (latent) {
+      u0 = draw_uniforms(A, st, 0, L).x;
+      eps0 = draw_normal(A, st, 0, L);
+    }
+  };
+  if (root) draws();
   if (!root) {
-    run_mlp<KM>(A, st, L);
+    run_mlp<KM>(A, st, L, draws);
     min_scale = t[0];
     // pi = softmax(logits).clamp_min(1e-5); pi /= sum (mdn.py:227-228)
     lmax = -INFINITY;
@@ -571,9 +670,9 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
                 : softplus_t(scr[(K + k * 2 * D + D + d) * WAVE + lane]) + min_scale;
   };
   if (latent) {
-    const int idx = inv_cdf(K, draw_uniforms(A, st, 0, L).x, pi_k);
+    const int idx = inv_cdf(K, u0, pi_k);
     for (int d = 0; d < D; ++d)
-      vwrite(L, st.out_col + d, loc_kd(idx, d) + draw_normal(A, st, d, L) * scale_kd(idx, d));
+      vwrite(L, st.out_col + d, loc_kd(idx, d) + (d == 0 ? eps0 : draw_normal(A, st, d, L)) * scale_kd(idx, d));
   } else {
     for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, node_fixed(A, st, d, L));
   }
@@ -632,7 +731,9 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
   const bool clip = (st.flags & VBN_F_CLIP) != 0;
   const int mode = st.aux0;
   const int lane = L.lane;
-  if (!root) run_mlp<KM>(A, st, L);
+  float2 uu0 = make_float2(0.f, 0.f);               // dim-0 uniforms
+  auto draws = [&]() { if (latent) uu0 = draw_uniforms(A, st, 0, L); };
+  if (root) draws(); else run_mlp<KM>(A, st, L, draws);
   float lp_acc = 0.f;
   for (int d = 0; d < D; ++d) {
     auto logit = [&](int c) -> float {
@@ -651,7 +752,7 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
     float x;
     int idx;
     if (latent) {
-      const float2 uu = draw_uniforms(A, st, d, L);
+      const float2 uu = d == 0 ? uu0 : draw_uniforms(A, st, d, L);
       idx = inv_cdf(C, uu.x, [&](int c) { return __expf(logit(c) - m) / se; });
       const float left = e[idx];
       const float right = e[idx + 1 < C ? idx + 1 : C];
@@ -1303,22 +1404,96 @@ __device__ __forceinline__ void gibbs_collect(const vbn_walk_args& A, const vbn_
 // ------------------------------------------------------------------------------------------
 // the walk
 // ------------------------------------------------------------------------------------------
+// One step of the walk for the wave's 64 particles.
 // KM: bit0 gaussian_nn, bit1 linear_gaussian, bit2 mdn, bit3 kde, bit4 softmax_nn,
 // bit5 non-relu activations.  Each instantiation only carries the code (and registers) of
 // the CPD kinds a plan uses.
 template <unsigned KM>
-__global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params,
-                                                        const vbn_step* __restrict__ steps,
-                                                        const int32_t* __restrict__ in_cols) {
+__device__ __forceinline__ void walk_step(const vbn_walk_args& A, const vbn_step& st, Lane& L, float& lp) {
+  if (st.role == VBN_ROLE_SKIP) return;
+  if (st.flags & VBN_F_LPRESET) lp = 0.f;
+  if (st.role == VBN_ROLE_SELECT) {
+    gibbs_select(A, st, L, lp);
+    wave_sync();
+    return;
+  }
+  if (st.role == VBN_ROLE_COLLECT) {
+    gibbs_collect(A, st, L);
+    return;
+  }
+  if (st.role == VBN_ROLE_FIXED && !(st.flags & VBN_F_LOGP)) {   // evidence / do: value only
+    for (int d = 0; d < st.out_dim; ++d) vwrite(L, st.out_col + d, node_fixed(A, st, d, L));
+    wave_sync();
+    return;
+  }
+  switch (st.kind) {
+    case VBN_KIND_GAUSSIAN_NN: if constexpr ((KM & 1) != 0) step_gaussian_nn<KM>(A, st, L, lp); break;
+    case VBN_KIND_LINEAR_GAUSSIAN: if constexpr ((KM & 2) != 0) step_linear_gaussian(A, st, L, lp); break;
+    case VBN_KIND_MDN: if constexpr ((KM & 4) != 0) step_mdn<KM>(A, st, L, lp); break;
+    case VBN_KIND_KDE: if constexpr ((KM & 8) != 0) step_kde(A, st, L, lp); break;
+    default: if constexpr ((KM & 16) != 0) step_softmax_nn<KM>(A, st, L, lp); break;
+  }
+  wave_sync();
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+// VBN_STAGE 1: NN weight blocks staged into LDS one step ahead, shared by the waves of a
+// workgroup; 0: every wave reads them straight from the blob (L1/L2)
+#ifndef VBN_STAGE
+#define VBN_STAGE 1
+#endif
+#define WG_MAX_WAVES (VBN_STAGE ? 4 : 1)
+#define WBLK_CHUNK 256   // floats per global_load_lds_dwordx4 wave instruction (64 lanes x 16 B)
+
+// Stage step j's NN weight block into LDS weight buffer ``buf``: the workgroup's waves split
+// its 1-KiB chunks, one global_load_lds_dwordx4 each (no VGPRs; completion is waited for by
+// step_barrier before the step that reads it).
+__device__ __forceinline__ void stage_block(const vbn_walk_args& A, const vbn_step* __restrict__ steps,
+                                            const float* __restrict__ params, float* wbuf, int j, int buf,
+                                            int wave, int nw, int lane) {
+  const int off = steps[j].reserved[5], len = steps[j].reserved[6];
+  if (len <= 0) return;
+  float* dst = wbuf + buf * A.wbuf_floats;
+  for (int c = wave; c * WBLK_CHUNK < len; c += nw)
+    __builtin_amdgcn_global_load_lds((const void*)(params + off + c * WBLK_CHUNK + lane * 4),
+                                     (lds_void*)(dst + c * WBLK_CHUNK), 16, 0, 0);
+}
+
+// end of a step: this wave's LDS-DMA has landed, every wave of the workgroup is done with the
+// buffer the next step's prefetch overwrites
+__device__ __forceinline__ void step_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef VBN_ABL_NOBAR
+  return;
+#endif
+  __syncthreads();
+}
+
+// The walk.  A workgroup = nw (1, 2 or 4; blockDim.x / 64) waves, each owning 64 consecutive
+// particles with its own LDS value slots; the waves walk the same step table in lockstep (one
+// barrier per step) and share two LDS weight buffers: while step i runs on buffer i & 1, step
+// i + 1's MLP weights are DMA'd into the other one (one memory latency per step, hidden
+// behind the step's compute, and one copy per workgroup instead of per wave).
+#ifndef VBN_WPE
+#define VBN_WPE 4
+#endif
+template <unsigned KM>
+__global__ void __launch_bounds__(WG_MAX_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(VBN_WPE)))
+vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const vbn_step* __restrict__ steps,
+                const int32_t* __restrict__ in_cols) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6;
+  const int per_wave = (A.n_slots + (A.max_out > 0 ? A.max_out : 1)) * WAVE;
+  float* wbuf = smem + nw * per_wave;
   Lane L;
   L.P = params;
   L.ic = in_cols;
-  L.lane = threadIdx.x;
-  L.vals = smem;
-  L.scr = smem + A.n_slots * WAVE;
+  L.lane = threadIdx.x & (WAVE - 1);
+  L.vals = smem + wave * per_wave;
+  L.scr = L.vals + A.n_slots * WAVE;
+  L.wb = wbuf;
   const int64_t total = A.n_queries * (int64_t)A.n_samples;
-  const int64_t p_raw = (int64_t)blockIdx.x * WAVE + L.lane;
+  const int64_t p_raw = ((int64_t)blockIdx.x * nw + wave) * WAVE + L.lane;
   const bool valid = p_raw < total;
   L.p = valid ? p_raw : total - 1;
   L.b = L.p / A.n_samples;
@@ -1333,36 +1508,32 @@ __global__ void __launch_bounds__(WAVE) __attribute__((amdgpu_waves_per_eu(4))) 
     wave_sync();
   }
   const int iters = A.mode == VBN_MODE_GIBBS ? A.gibbs_iters : 1;
+#if VBN_STAGE
+  int par = 0;
+  if (A.n_steps > 0) stage_block(A, steps, params, wbuf, 0, 0, wave, nw, L.lane);
+  step_barrier();
   for (int it = 0; it < iters; ++it) {
-  L.iter = it;
-  for (int i = 0; i < A.n_steps; ++i) {
-    const vbn_step st = steps[i];
-    if (st.role == VBN_ROLE_SKIP) continue;
-    if (st.flags & VBN_F_LPRESET) lp = 0.f;
-    if (st.role == VBN_ROLE_SELECT) {
-      gibbs_select(A, st, L, lp);
-      wave_sync();
-      continue;
+    L.iter = it;
+    for (int i = 0; i < A.n_steps; ++i) {
+      const bool last = i + 1 == A.n_steps;
+      if (!last || it + 1 < iters) stage_block(A, steps, params, wbuf, last ? 0 : i + 1, par ^ 1, wave, nw, L.lane);
+      L.wb = wbuf + par * A.wbuf_floats;
+      walk_step<KM>(A, steps[i], L, lp);
+      step_barrier();
+      par ^= 1;
     }
-    if (st.role == VBN_ROLE_COLLECT) {
-      gibbs_collect(A, st, L);
-      continue;
-    }
-    if (st.role == VBN_ROLE_FIXED && !(st.flags & VBN_F_LOGP)) {   // evidence / do: value only
-      for (int d = 0; d < st.out_dim; ++d) vwrite(L, st.out_col + d, node_fixed(A, st, d, L));
-      wave_sync();
-      continue;
-    }
-    switch (st.kind) {
-      case VBN_KIND_GAUSSIAN_NN: if constexpr ((KM & 1) != 0) step_gaussian_nn<KM>(A, st, L, lp); break;
-      case VBN_KIND_LINEAR_GAUSSIAN: if constexpr ((KM & 2) != 0) step_linear_gaussian(A, st, L, lp); break;
-      case VBN_KIND_MDN: if constexpr ((KM & 4) != 0) step_mdn<KM>(A, st, L, lp); break;
-      case VBN_KIND_KDE: if constexpr ((KM & 8) != 0) step_kde(A, st, L, lp); break;
-      default: if constexpr ((KM & 16) != 0) step_softmax_nn<KM>(A, st, L, lp); break;
-    }
-    wave_sync();
   }
+#else
+  (void)wbuf;
+  for (int it = 0; it < iters; ++it) {
+    L.iter = it;
+    for (int i = 0; i < A.n_steps; ++i) {
+      const vbn_step st = steps[i];
+      L.wb = params + st.reserved[5];
+      walk_step<KM>(A, st, L, lp);
+    }
   }
+#endif
   if (!valid) return;
   if (A.mode == VBN_MODE_GIBBS) return;                  // outputs written by COLLECT steps
   if (A.state && (A.state_flags & 2)) {
@@ -1678,14 +1849,27 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
     return fail(VBN_E_ARGS, "vbn_hip_walk: bad arguments");
   if (a->out_x && (!a->out_cols || a->n_out_cols <= 0))
     return fail(VBN_E_ARGS, "vbn_hip_walk: out_x without out_cols");
-  const int64_t lds = vbn_hip_lds_bytes(a->n_slots, a->max_out);
-  if (lds > 160 * 1024) return fail(VBN_E_LDS, "vbn_hip_walk: plan needs more than 160 KiB of LDS per wave");
+  if (a->wbuf_floats < 0 || (a->wbuf_floats % WBLK_CHUNK) != 0)
+    return fail(VBN_E_ARGS, "vbn_hip_walk: wbuf_floats must be a non-negative multiple of 256");
+  // waves per workgroup: the most resident waves per CU (160 KiB LDS, 16 waves = 4 per SIMD at
+  // the kernel's register budget), larger workgroups on ties (one weight copy per workgroup)
+  const int64_t per_wave = vbn_hip_lds_bytes(a->n_slots, a->max_out);
+  const int64_t wbuf_bytes = VBN_STAGE ? 2 * (int64_t)a->wbuf_floats * (int64_t)sizeof(float) : 0;
+  int nw = 0;
+  int64_t lds = 0, best = 0;
+  for (int w = WG_MAX_WAVES; w >= 1; w >>= 1) {
+    const int64_t l = w * per_wave + wbuf_bytes;
+    if (l > 160 * 1024) continue;
+    const int64_t res = std::min<int64_t>(16, (160 * 1024 / l) * w);
+    if (res > best) { best = res; nw = w; lds = l; }
+  }
+  if (nw == 0) return fail(VBN_E_LDS, "vbn_hip_walk: plan needs more than 160 KiB of LDS per wave");
   if (a->mode == VBN_MODE_GIBBS &&
       (a->n_samples != 8 || a->gibbs_iters <= 0 || a->gibbs_burn_in < 0 || a->gibbs_burn_in >= a->gibbs_iters ||
        a->gibbs_thin <= 0 || !a->out_x || (a->noise && a->n_noise <= 0)))
     return fail(VBN_E_ARGS, "vbn_hip_walk: Gibbs walk needs 8 candidates, iters > burn_in >= 0, thin > 0, out_x");
   const int64_t total = a->n_queries * (int64_t)a->n_samples;
-  const int64_t blocks = (total + WAVE - 1) / WAVE;
+  const int64_t blocks = (total + (int64_t)WAVE * nw - 1) / ((int64_t)WAVE * nw);
   if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
   // smallest instantiated kind set covering the plan
   static const unsigned masks[] = {1u, 2u, 3u, 4u, 8u, 16u, 20u, 23u, 31u, 63u};
@@ -1694,8 +1878,14 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   for (unsigned m : masks) {
     if ((m & want) == want && __builtin_popcount(m) < __builtin_popcount(km)) km = m;
   }
-  const dim3 grid((unsigned)blocks), block(WAVE);
+  const dim3 grid((unsigned)blocks), block(WAVE * nw);
   hipStream_t st = (hipStream_t)stream;
+#ifdef VBN_KM_ONLY
+  // experiment builds (make exp KM=...): one instantiation only
+  if ((VBN_KM_ONLY & want) != want) return fail(VBN_E_ARGS, "vbn_hip_walk: kind set not built in this experiment library");
+  hipLaunchKernelGGL(vbn_walk_kernel<(unsigned)VBN_KM_ONLY>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols);
+  (void)km;
+#else
   switch (km) {
     case 1u: hipLaunchKernelGGL(vbn_walk_kernel<1u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
     case 2u: hipLaunchKernelGGL(vbn_walk_kernel<2u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
@@ -1708,6 +1898,7 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
     case 31u: hipLaunchKernelGGL(vbn_walk_kernel<31u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
     default: hipLaunchKernelGGL(vbn_walk_kernel<63u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
   }
+#endif
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;

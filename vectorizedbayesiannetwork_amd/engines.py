@@ -209,9 +209,9 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
             len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
             plan.mode != MODE_SAMPLE, plan.kind_mask)
     if state is None:
-        lp, x = ops.walk(*args)
+        lp, x = ops.walk(*args, plan.wbuf)
     else:
-        lp, x = ops.walk_segment(*args, state, state_flags, step_begin, step_end)
+        lp, x = ops.walk_segment(*args, state, state_flags, step_begin, step_end, plan.wbuf)
     if plan.mode != MODE_SAMPLE:
         lp = lp.view(b, n)
     if n_out_cols:
@@ -642,7 +642,7 @@ class GibbsSampler(_EngineBase):
         out = ops.gibbs_walk(gp.steps, gp.in_cols, pk.params, fx,
                              sweep_noise, chains.contiguous(), b, init.n_slots, init.max_out, init.fixed_ld,
                              noise_b, gp.n_noise, pk.dmax, dt, iters, burn, th, self.q_base, seed, 1,
-                             gp.kind_mask)
+                             gp.kind_mask, gp.wbuf)
         if self.collect == "chain" and n > 0:
             return out
         return out.expand(b, max(n, 1), dt).contiguous()

@@ -44,11 +44,12 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
          out_cols: Tensor, n_queries: int, n_samples: int, n_slots: int, max_out: int,
          fixed_ld: int, fixed_per_particle: bool, noise_b: int, n_noise: int, dmax: int,
          n_out_cols: int, mode: int, q_base: int, seed: int, offset: int,
-         want_lp: bool, kind_mask: int = 63) -> Tuple[Tensor, Tensor]:
-    """One particle walk over the whole step table."""
+         want_lp: bool, kind_mask: int = 63, wbuf: int = 0) -> Tuple[Tensor, Tensor]:
+    """One particle walk over the whole step table (``wbuf``: floats per LDS weight buffer,
+    >= every step's weight-block length)."""
     return _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots,
                         max_out, fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode,
-                        q_base, seed, offset, want_lp, kind_mask, None, 0, 0, -1)
+                        q_base, seed, offset, want_lp, kind_mask, None, 0, 0, -1, wbuf)
 
 
 @torch.library.custom_op("vbn_hip::walk_segment", mutates_args=("state",))
@@ -57,25 +58,26 @@ def walk_segment(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, 
                  fixed_ld: int, fixed_per_particle: bool, noise_b: int, n_noise: int, dmax: int,
                  n_out_cols: int, mode: int, q_base: int, seed: int, offset: int,
                  want_lp: bool, kind_mask: int, state: Tensor, state_flags: int, step_begin: int,
-                 step_end: int) -> Tuple[Tensor, Tensor]:
+                 step_end: int, wbuf: int = 0) -> Tuple[Tensor, Tensor]:
     """One segment steps[step_begin:step_end] of a split walk; ``state`` [n_slots + 1, B*S]
     carries node values and log-weights between segments (state_flags 1 = load, 2 = store)."""
     return _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots,
                         max_out, fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode,
-                        q_base, seed, offset, want_lp, kind_mask, state, state_flags, step_begin, step_end)
+                        q_base, seed, offset, want_lp, kind_mask, state, state_flags, step_begin, step_end,
+                        wbuf)
 
 
 @walk_segment.register_fake
 def _walk_segment_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                        fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
-                       offset, want_lp, kind_mask, state, state_flags, step_begin, step_end):
+                       offset, want_lp, kind_mask, state, state_flags, step_begin, step_end, wbuf=0):
     total = n_queries * n_samples
     return params.new_empty(total if want_lp else 0), params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))
 
 
 def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                  fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
-                 offset, want_lp, kind_mask, state, state_flags, step_begin, step_end):
+                 offset, want_lp, kind_mask, state, state_flags, step_begin, step_end, wbuf):
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::walk runs on the GPU only (no CPU fallback); "
@@ -133,6 +135,7 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
     a.q_base = q_base
     a.seed = seed & ((1 << 64) - 1)
     a.offset = offset & ((1 << 64) - 1)
+    a.wbuf_floats = int(wbuf)
     lib = _lib.load()
     with torch.cuda.device(device):
         _lib.check(lib.vbn_hip_walk(ctypes.byref(a), ctypes.c_void_p(_stream_handle(device))), "vbn_hip_walk")
@@ -142,7 +145,7 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
 @walk.register_fake
 def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
-               offset, want_lp, kind_mask=63):
+               offset, want_lp, kind_mask=63, wbuf=0):
     total = n_queries * n_samples
     lp = params.new_empty(total if want_lp else 0)
     x = params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))
@@ -153,7 +156,7 @@ def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samp
 def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: Optional[Tensor],
                state: Tensor, n_queries: int, n_slots: int, max_out: int, fixed_ld: int, noise_b: int,
                n_noise: int, dmax: int, out_dim: int, iters: int, burn_in: int, thin: int, q_base: int,
-               seed: int, offset: int, kind_mask: int) -> Tensor:
+               seed: int, offset: int, kind_mask: int, wbuf: int = 0) -> Tensor:
     """``iters`` Gibbs sweeps (gibbs.py:34-87) over B chains x 8 candidate lanes, started from
     ``state`` [n_slots + 1, B*8]; returns the collected target values [B, n_collect, out_dim]."""
     device = params.device
@@ -210,6 +213,7 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
     a.gibbs_burn_in = burn_in
     a.gibbs_thin = thin
     a.n_noise = n_noise
+    a.wbuf_floats = int(wbuf)
     lib = _lib.load()
     with torch.cuda.device(device):
         _lib.check(lib.vbn_hip_walk(ctypes.byref(a), ctypes.c_void_p(_stream_handle(device))), "vbn_hip_walk")
@@ -218,7 +222,7 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
 
 @gibbs_walk.register_fake
 def _gibbs_walk_fake(steps, in_cols, params, fixed, noise, state, n_queries, n_slots, max_out, fixed_ld,
-                     noise_b, n_noise, dmax, out_dim, iters, burn_in, thin, q_base, seed, offset, kind_mask):
+                     noise_b, n_noise, dmax, out_dim, iters, burn_in, thin, q_base, seed, offset, kind_mask, wbuf=0):
     return params.new_empty((n_queries, (iters - burn_in + thin - 1) // thin, out_dim))
 
 

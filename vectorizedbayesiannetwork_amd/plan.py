@@ -37,7 +37,9 @@ MODE_MCM, MODE_WEIGHTED, MODE_SAMPLE, MODE_GIBBS = 0, 1, 2, 3
 STEP_INTS = 32
 (S_KIND, S_ROLE, S_FLAGS, S_ACT, S_NIN, S_INOFF, S_OUTCOL, S_OUTDIM, S_FIXEDCOL, S_K, S_NOUT,
  S_NODEID, S_NOISE, S_AUX0, S_AUX1, S_AUX2, S_OFF_STD, S_OFF_W1, S_OFF_W2, S_OFF_B2, S_OFF_W3,
- S_OFF_B3, S_OFF_TAIL, S_OFF_PTS, S_OFF_W2H, S_OFF_KQ, S_OFF_KQY, S_OFF_KR, S_OFF_KV) = range(29)
+ S_OFF_B3, S_OFF_TAIL, S_OFF_PTS, S_OFF_W2H, S_OFF_KQ, S_OFF_KQY, S_OFF_KR, S_OFF_KV,
+ S_WBLK_OFF, S_WBLK_LEN) = range(31)
+WBLK_CHUNK = 256          # floats per LDS-DMA wave instruction (64 lanes x 16 B)
 KDE_CHUNKS = 16
 MLP_HIDDEN = (32, 32)
 KDE_MAX_DIMS = 4
@@ -69,7 +71,8 @@ class _Blob:
         return off
 
     def finish(self) -> np.ndarray:
-        return np.concatenate(self.parts) if self.parts else np.zeros(4, np.float32)
+        # one DMA chunk of slack: a weight block's last 1 KiB chunk may read past its end
+        return np.concatenate(self.parts + [np.zeros(WBLK_CHUNK, np.float32)])
 
 
 _KDE_C = math.sqrt(0.5 * math.log2(math.e))      # exp(-d^2 / 2) = exp2(-(c d)^2)
@@ -145,13 +148,15 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     w1z[:, :nin] = w1
     lane = np.arange(64)
     w1f = np.stack([w1z[lane & 31, 2 * t + (lane >> 5)] for t in range(t1)])   # [t1, 64]
-    offs["w1"] = blob.add(w1f)
-    # accumulator init: [layer][group g][half h][register r] = b[row(r, h)] (one copy per group)
-    offs["b2"] = blob.add(np.stack([np.stack([b[_ROWS]] * 2) for b in (b1, b2)]))  # [2, 2, 2, 16]
     w2f = np.zeros((16, 64), np.float32)
     for s in range(16):
         w2f[s] = w2[lane & 31, _ROWS[lane >> 5, s]]
-    offs["w2"] = blob.add(w2f.reshape(4, 4, 64).transpose(0, 2, 1))            # [4, 64, 4] (exact f32)
+    # weight block staged into LDS by the walk (one step ahead): W1 | biases | split-f16 W2,
+    # contiguous, 16-byte aligned pieces
+    offs["w1"] = blob.add(w1f)
+    offs["wblk"] = offs["w1"]
+    # accumulator init: [layer][group g][half h][register r] = b[row(r, h)] (one copy per group)
+    offs["b2"] = blob.add(np.stack([np.stack([b[_ROWS]] * 2) for b in (b1, b2)]))  # [2, 2, 2, 16]
     # split-f16 fragments of v_mfma_f32_32x32x16_f16: k-step s, lane l, element j ->
     # W2[l&31][16s + 8(j>>2) + 4(l>>5) + (j&3)]; hi = f16(w), lo = f16(w - hi)
     if np.abs(w2).max() > 32768.0:
@@ -165,8 +170,12 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     lo = (frag - hi.astype(np.float32)).astype(np.float16)
     halfs = np.concatenate([hi, lo]).reshape(-1)                               # [4, 64, 8] f16
     offs["w2h"] = blob.add(halfs.view(np.float32))
+    # head: row j = W3[j][row(r, 0)] (r < 16) ++ W3[j][row(r, 1)] (lane half h reads 16 at 16 h)
     offs["w3"] = blob.add(np.concatenate([w3[:, _ROWS[0]], w3[:, _ROWS[1]]], axis=1))  # [n_out, 32]
     offs["b3"] = blob.add(b3)
+    blen = offs["b3"] + b3.size - offs["wblk"]
+    offs["wblk_len"] = -(-blen // WBLK_CHUNK) * WBLK_CHUNK
+    offs["w2"] = blob.add(w2f.reshape(4, 4, 64).transpose(0, 2, 1))            # [4, 64, 4] (exact f32)
     offs["n_out"] = w3.shape[0]
     return offs
 
@@ -344,6 +353,7 @@ class QueryPlan:
     mode: int
     slot_of: Dict[str, int]
     kind_mask: int = 63       # CPD kinds the walk evaluates (selects the kernel instantiation)
+    wbuf: int = 0             # floats per LDS weight buffer (max wblk_len over the steps)
 
 
 def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
@@ -484,6 +494,9 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         row[S_OFF_KQY] = npk.offs.get("kqy", -1)
         row[S_OFF_KR] = npk.offs.get("kr", -1)
         row[S_OFF_KV] = npk.offs.get("kv", -1)
+        if "wblk" in npk.offs and (n in latent_s or n in logp_s or n in params_s):
+            row[S_WBLK_OFF] = npk.offs["wblk"]
+            row[S_WBLK_LEN] = npk.offs["wblk_len"]
     out_cols: List[int] = []
     for n in out_nodes:
         out_cols.extend(range(slot_of[n], slot_of[n] + width(n)))
@@ -507,7 +520,8 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         steps=torch.from_numpy(steps).to(dev) if len(order) else torch.zeros(1, STEP_INTS, dtype=torch.int32, device=dev),
         in_cols=t(in_cols), out_cols=t(out_cols), n_steps=len(order), n_slots=max(n_slots, 1),
         max_out=max_out, fixed_nodes=fixed_nodes, fixed_ld=max(c, 1), noise_nodes=noise_nodes,
-        out_nodes=list(out_nodes), mode=mode, slot_of=slot_of, kind_mask=kind_mask)
+        out_nodes=list(out_nodes), mode=mode, slot_of=slot_of, kind_mask=kind_mask,
+        wbuf=int(steps[:, S_WBLK_LEN].max()) if len(order) else 0)
 
 
 @dataclass
@@ -520,6 +534,7 @@ class GibbsPlan:
     n_noise: int
     in_cols: torch.Tensor      # parent slots of every row (children read their parents too)
     kind_mask: int
+    wbuf: int = 0              # floats per LDS weight buffer (max wblk_len over the sweep steps)
 
 
 def build_gibbs_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[str], target: str,
@@ -568,6 +583,11 @@ def build_gibbs_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Seque
     r[S_ROLE] = ROLE_COLLECT
     r[S_FLAGS] = 0
     table.append(r)
-    steps = torch.from_numpy(np.ascontiguousarray(np.stack(table))).to(packed.device)
+    tab = np.ascontiguousarray(np.stack(table))
+    sel = (tab[:, S_ROLE] == ROLE_SELECT) | (tab[:, S_ROLE] == ROLE_COLLECT)
+    tab[sel, S_WBLK_OFF] = 0                                              # no MLP on these rows
+    tab[sel, S_WBLK_LEN] = 0
+    steps = torch.from_numpy(tab).to(packed.device)
     return GibbsPlan(init=init, steps=steps, n_steps=len(table), latent=lat, target=target,
-                     n_noise=max(2 * len(lat), 1), in_cols=full.in_cols, kind_mask=full.kind_mask)
+                     n_noise=max(2 * len(lat), 1), in_cols=full.in_cols, kind_mask=full.kind_mask,
+                     wbuf=int(tab[:, S_WBLK_LEN].max()))
