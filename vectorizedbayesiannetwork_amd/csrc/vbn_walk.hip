@@ -328,6 +328,43 @@ __device__ __forceinline__ f32x16 layer2_exact(const vbn_step& st, const Lane& L
   return b;
 }
 
+// Head outputs two at a time (both outputs' weights in flight together; w3/b3 (weight block)
+// and scr (head scratch) are distinct LDS rows, so the reads need not wait for the writes).
+__device__ __forceinline__ float head_dot(const float4 (&w)[4], const float (&y0)[16], const float (&y1)[16],
+                                          float b, bool nan_in) {
+  float a0 = 0.f, c0 = 0.f, a1 = 0.f, c1 = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a0 = fmaf(w[q].x, y0[4 * q], a0);
+    c0 = fmaf(w[q].y, y0[4 * q + 1], c0);
+    a1 = fmaf(w[q].x, y1[4 * q], a1);
+    c1 = fmaf(w[q].y, y1[4 * q + 1], c1);
+    a0 = fmaf(w[q].z, y0[4 * q + 2], a0);
+    c0 = fmaf(w[q].w, y0[4 * q + 3], c0);
+    a1 = fmaf(w[q].z, y1[4 * q + 2], a1);
+    c1 = fmaf(w[q].w, y1[4 * q + 3], c1);
+  }
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0 + c0), __float_as_uint(a1 + c1), false, false);
+  const float o = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + b;
+  return nan_in ? __int_as_float(0x7fc00000) : o;
+}
+
+__device__ __forceinline__ void head_outputs(const float* __restrict__ w3, const float* __restrict__ b3,
+                                             float* __restrict__ scr, int nout, const float (&y0)[16],
+                                             const float (&y1)[16], bool nan_in) {
+#pragma clang loop unroll(disable)
+  for (int j = 0; j < nout; j += 2) {
+    const bool two = j + 1 < nout;
+    const float4* wa = reinterpret_cast<const float4*>(w3 + 32 * j);
+    const float4* wb = reinterpret_cast<const float4*>(w3 + 32 * (two ? j + 1 : j));
+    const float4 va[4] = {wa[0], wa[1], wa[2], wa[3]};
+    const float4 vb[4] = {wb[0], wb[1], wb[2], wb[3]};
+    const float ba = b3[j], bb = b3[two ? j + 1 : j];
+    scr[j * WAVE] = head_dot(va, y0, y1, ba, nan_in);
+    if (two) scr[(j + 1) * WAVE] = head_dot(vb, y0, y1, bb, nan_in);
+  }
+}
+
 // Head on VALU in the accumulator layout (no transpose): lane half h holds hidden rows
 // row(r, h) of its particle, so per output j the half's 16 products use per-lane weights
 // W3[j][row(r, h)] (the pack's [n_out][32] rows hold 16 per half), in two independent chains
@@ -349,30 +386,8 @@ __device__ __forceinline__ void mlp_head(const vbn_step& st, const Lane& L, cons
     y0[r] = act_fn<ACT>(h0[r]);
     y1[r] = act_fn<ACT>(h1[r]);
   }
-  const int nout = st.n_out;
-  const float* __restrict__ w3 = W + (st.off_w3 - WBLK_OFF(st)) + 16 * (lane >> 5);
-  const float* __restrict__ b3 = W + (st.off_b3 - WBLK_OFF(st));
-#pragma clang loop unroll(disable)
-  for (int j = 0; j < nout; ++j) {
-    const float4* w4 = reinterpret_cast<const float4*>(w3 + 32 * j);
-    float wv[16];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 v = w4[q];
-      wv[4 * q] = v.x; wv[4 * q + 1] = v.y; wv[4 * q + 2] = v.z; wv[4 * q + 3] = v.w;
-    }
-    float a0 = 0.f, c0 = 0.f, a1 = 0.f, c1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      a0 = fmaf(wv[r], y0[r], a0);
-      c0 = fmaf(wv[r + 1], y0[r + 1], c0);
-      a1 = fmaf(wv[r], y1[r], a1);
-      c1 = fmaf(wv[r + 1], y1[r + 1], c1);
-    }
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0 + c0), __float_as_uint(a1 + c1), false, false);
-    const float o = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + b3[j];
-    L.scr[j * WAVE + lane] = nan_in ? __int_as_float(0x7fc00000) : o;
-  }
+  head_outputs(W + (st.off_w3 - WBLK_OFF(st)) + 16 * (lane >> 5), W + (st.off_b3 - WBLK_OFF(st)),
+               L.scr + lane, st.n_out, y0, y1, nan_in);
   wave_sync();
 }
 
@@ -1437,12 +1452,16 @@ __device__ __forceinline__ void walk_step(const vbn_walk_args& A, const vbn_step
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
-// VBN_STAGE 1: NN weight blocks staged into LDS one step ahead, shared by the waves of a
-// workgroup; 0: every wave reads them straight from the blob (L1/L2)
+// Staged walks (kind sets of gaussian_nn / linear_gaussian only): NN weight blocks are DMA'd
+// into LDS one step ahead and shared by the 4 waves of a workgroup, one barrier per step.
+// Measured on MI355X (walk ms, staged vs direct): cfg2 1.22 vs 1.35; with mdn/softmax_nn heads
+// (cfg3) 4.43 vs 4.26 and with KDE nodes (cfg5) 186 vs 166 (per-wave work varies by node, the
+// barrier waits for the slowest wave) -- those kind sets read the blob straight (L1/L2).
 #ifndef VBN_STAGE
 #define VBN_STAGE 1
 #endif
-#define WG_MAX_WAVES (VBN_STAGE ? 4 : 1)
+__host__ __device__ constexpr bool staged_kinds(unsigned km) { return VBN_STAGE && (km & 28u) == 0; }
+#define WG_MAX_WAVES 4
 #define WBLK_CHUNK 256   // floats per global_load_lds_dwordx4 wave instruction (64 lanes x 16 B)
 
 // Stage step j's NN weight block into LDS weight buffer ``buf``: the workgroup's waves split
@@ -1508,7 +1527,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
     wave_sync();
   }
   const int iters = A.mode == VBN_MODE_GIBBS ? A.gibbs_iters : 1;
-#if VBN_STAGE
+  if constexpr (staged_kinds(KM)) {
   int par = 0;
   if (A.n_steps > 0) stage_block(A, steps, params, wbuf, 0, 0, wave, nw, L.lane);
   step_barrier();
@@ -1523,7 +1542,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
       par ^= 1;
     }
   }
-#else
+  } else {
   (void)wbuf;
   for (int it = 0; it < iters; ++it) {
     L.iter = it;
@@ -1533,7 +1552,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
       walk_step<KM>(A, st, L, lp);
     }
   }
-#endif
+  }
   if (!valid) return;
   if (A.mode == VBN_MODE_GIBBS) return;                  // outputs written by COLLECT steps
   if (A.state && (A.state_flags & 2)) {
@@ -1851,13 +1870,25 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
     return fail(VBN_E_ARGS, "vbn_hip_walk: out_x without out_cols");
   if (a->wbuf_floats < 0 || (a->wbuf_floats % WBLK_CHUNK) != 0)
     return fail(VBN_E_ARGS, "vbn_hip_walk: wbuf_floats must be a non-negative multiple of 256");
-  // waves per workgroup: the most resident waves per CU (160 KiB LDS, 16 waves = 4 per SIMD at
-  // the kernel's register budget), larger workgroups on ties (one weight copy per workgroup)
+  // smallest instantiated kind set covering the plan
+  static const unsigned masks[] = {1u, 2u, 3u, 4u, 8u, 16u, 20u, 23u, 31u, 63u};
+  const unsigned want = (unsigned)a->kind_mask & 63u;
+  unsigned km = 63u;
+  for (unsigned m : masks) {
+    if ((m & want) == want && __builtin_popcount(m) < __builtin_popcount(km)) km = m;
+  }
+#ifdef VBN_KM_ONLY
+  km = VBN_KM_ONLY;
+#endif
+  // waves per workgroup: staged kind sets take the most resident waves per CU (160 KiB LDS,
+  // 16 waves = 4 per SIMD at the kernel's register budget), larger workgroups on ties (one
+  // weight copy per workgroup); the other kind sets run one wave per workgroup
   const int64_t per_wave = vbn_hip_lds_bytes(a->n_slots, a->max_out);
-  const int64_t wbuf_bytes = VBN_STAGE ? 2 * (int64_t)a->wbuf_floats * (int64_t)sizeof(float) : 0;
+  const bool stage = staged_kinds(km);
+  const int64_t wbuf_bytes = stage ? 2 * (int64_t)a->wbuf_floats * (int64_t)sizeof(float) : 0;
   int nw = 0;
   int64_t lds = 0, best = 0;
-  for (int w = WG_MAX_WAVES; w >= 1; w >>= 1) {
+  for (int w = stage ? WG_MAX_WAVES : 1; w >= 1; w >>= 1) {
     const int64_t l = w * per_wave + wbuf_bytes;
     if (l > 160 * 1024) continue;
     const int64_t res = std::min<int64_t>(16, (160 * 1024 / l) * w);
@@ -1871,13 +1902,6 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   const int64_t total = a->n_queries * (int64_t)a->n_samples;
   const int64_t blocks = (total + (int64_t)WAVE * nw - 1) / ((int64_t)WAVE * nw);
   if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
-  // smallest instantiated kind set covering the plan
-  static const unsigned masks[] = {1u, 2u, 3u, 4u, 8u, 16u, 20u, 23u, 31u, 63u};
-  const unsigned want = (unsigned)a->kind_mask & 63u;
-  unsigned km = 63u;
-  for (unsigned m : masks) {
-    if ((m & want) == want && __builtin_popcount(m) < __builtin_popcount(km)) km = m;
-  }
   const dim3 grid((unsigned)blocks), block(WAVE * nw);
   hipStream_t st = (hipStream_t)stream;
 #ifdef VBN_KM_ONLY
