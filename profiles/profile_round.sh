@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=${1:-gpurun_out/prof}
 CFG=${2:-cfg2}
 mkdir -p $OUT
-B="bench.py --config $CFG --steps ${STEPS:-5} --warmup 1 --no-cpu-baseline"
+B="bench.py --config $CFG --steps ${STEPS:-5} --warmup ${WARMUP:-1} --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $B > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $B > $OUT/pmc_write.log 2>&1
