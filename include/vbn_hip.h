@@ -105,7 +105,8 @@ enum vbn_mode {
  * reserved[0] = split-f16 W2 fragments; [1..4] = KDE point packs; [5] = wblk_off, [6] =
  * wblk_len: the NN CPD's weight block [W1 fragments | accumulator-init biases | split-f16 W2]
  * (params float offset, length in floats, a multiple of 256), which the walk stages into LDS
- * one step ahead (0 = the step runs no MLP). */
+ * one step ahead (0 = the step runs no MLP); [7] = one-feature KDE point pack in the
+ * v_mfma_f32_32x32x2_f32 operand layout ([rows/32][2][32]: scaled point, |point|^2), or -1. */
 typedef struct vbn_step {
   int32_t kind, role, flags, act;
   int32_t n_in, in_off, out_col, out_dim;

@@ -319,3 +319,32 @@ def test_kde_mfma_pack_gives_kernel_weights(nf):
     ref = np.exp(-0.5 * ((parts[:, None, :].astype(np.float64) - pts[None].astype(np.float64)) ** 2).sum(-1) / s ** 2)
     np.testing.assert_allclose(w[:, :m], ref, rtol=1e-5, atol=1e-30)
     assert (w[:, m:] == 0).all()
+
+
+def test_kde_pack32_gives_kernel_weights():
+    """The one-feature 32x32x2 pack (plan._kde_pack32) in the v_mfma_f32_32x32x2_f32 operand
+    layout (A[m = l & 31][k = l >> 5] from pack[block][k][32]; B = (2x', -1); C = -|x'|^2,
+    k-ordered fmaf chain from C as csrc kde_arg_rec(nf < 0) replicates it) gives
+    exp2(d) = exp(-|x - y|^2 / (2 s^2)); padding points weigh 0; chunk rows match _kde_pack."""
+    from vectorizedbayesiannetwork_amd.plan import _KDE_C, _kde_cb, _kde_pack, _kde_pack32, KDE_CHUNKS
+    rng = np.random.default_rng(5)
+    m, s = 77, 0.6
+    c = np.float32(_KDE_C / s)
+    pts = rng.normal(size=(m, 1)).astype(np.float32)
+    parts = rng.normal(size=(64, 1)).astype(np.float32)
+    pk = _kde_pack32(pts * c)
+    rows = KDE_CHUNKS * _kde_cb(m) * 16
+    assert pk.shape == (rows // 32, 2, 32) and _kde_pack([pts * c]).shape[0] * 16 == rows
+    x = (parts * c)[:, 0].astype(np.float32)
+    w = np.zeros((64, rows))
+    for b in range(rows // 32):
+        a = pk[b].reshape(-1)                                    # lane l reads a[l]
+        for p in range(64):
+            negsq = np.float32(-np.float32(x[p] * x[p]))
+            for r in range(32):
+                d = np.float32(np.float32(a[r] * np.float32(2 * x[p])) + negsq)
+                d = np.float32(d - a[32 + r])
+                w[p, b * 32 + r] = 2.0 ** float(d)
+    ref = np.exp(-0.5 * ((parts[:, None, 0].astype(np.float64) - pts[None, :, 0]) ** 2) / s ** 2)
+    np.testing.assert_allclose(w[:, :m], ref, rtol=1e-5, atol=1e-30)
+    assert (w[:, m:] == 0).all()

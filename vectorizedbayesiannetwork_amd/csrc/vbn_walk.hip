@@ -931,6 +931,7 @@ __device__ __forceinline__ float kde_own(const Lane& L, const int (&slots)[4], c
 // (y'_0 .. y'_{nf-1}, |y'|^2, ..) of the per-point record pack.
 __device__ __forceinline__ float kde_arg_rec(const float4 r, float xb0, float xb1, float xb2, float negsq,
                                              int nf) {
+  if (nf < 0) return fmaf(r.y, -1.f, fmaf(r.x, xb0, negsq));   // one-feature 32x32x2 chain from C
   const bool zc = nf <= 2;
   float d = zc ? 0.f : negsq;
   d = fmaf(r.x, xb0, d);
@@ -1001,6 +1002,32 @@ __device__ __forceinline__ void kde_sums(const float* __restrict__ kq, int b0, i
 // Latent non-root KDE node, parent dims 1..3: index ~ softmax_j log K_p (kde.py:172-178).
 // Pass 1 (MFMA): per-chunk weight sums -> scr[chunk][lane]; pass 2 (VALU replica): locate the
 // chunk holding u * total, scan it.  All-underflow particles (every weight 0) redo the sums on
+// One-feature nodes: pass-1 sums on v_mfma_f32_32x32x2_f32 (1024 pairs per instruction, half
+// the matrix-pipe time of the 16x16x4 form): rows = 32 points (A = (y', |y'|^2), pack kq32
+// [block32][2][32]), columns = the 32 particles of tile t (B = (2x', -1)), C = -|x'|^2, i.e.
+// d = fmaf(|y'|^2, -1, fmaf(y', 2x', -|x'|^2)) (kde_arg_rec with nf < 0 replicates it).  Lane
+// (h, n) sums the exps of rows row(r, h) for particle 32 t + n; the two halves of both tiles
+// are added with one v_permlane32_swap per chunk.
+__device__ __forceinline__ void kde_mfma32_sums(const float* __restrict__ kq32, int b0, int b1, float bt0, float bt1,
+                                                float ct0, float ct1, int lane, float (&s)[2]) {
+  f32x16 c0, c1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { c0[r] = ct0; c1[r] = ct1; }
+  f32x2 acc0 = f32x2{0.f, 0.f}, acc1 = f32x2{0.f, 0.f};
+  for (int b = b0; b < b1; ++b) {
+    const float a = kq32[b * 64 + lane];
+    const f32x16 d0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt0, c0, 0, 0, 0);
+    const f32x16 d1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt1, c1, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      acc0 += f32x2{__builtin_amdgcn_exp2f(d0[r]), __builtin_amdgcn_exp2f(d0[r + 1])};
+      acc1 += f32x2{__builtin_amdgcn_exp2f(d1[r]), __builtin_amdgcn_exp2f(d1[r + 1])};
+    }
+  }
+  s[0] += acc0.x + acc0.y;
+  s[1] += acc1.x + acc1.y;
+}
+
 // VALU relative to their largest weight.
 __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
                                               float ucat, float c_p) {
@@ -1010,32 +1037,50 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   int slots[4] = {0, 0, 0, 0};
   float scl[4] = {c_p, c_p, c_p, c_p};
   for (int f = 0; f < nf; ++f) slots[f] = L.ic[st.in_off + f];
-  KdeOps o;
-  kde_operands(L, slots, scl, nf, o);
+  const bool k32 = nf == 1 && st.reserved[7] >= 0;   // one-feature node with the 32x32x2 pack
   double tot = 0.0;
-  for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    kde_sums(kq, ch * cb, ch * cb + cb, o, nf, lane, s);
-    const float cs = kde_reduce_tiles(s, lane);
-    L.scr[ch * WAVE + lane] = cs;
-    tot += (double)cs;
+  if (k32) {
+    const float* __restrict__ kq32 = L.P + st.reserved[7];
+    const int h = lane >> 5, n = lane & 31;
+    const float v0 = c_p * L.vals[slots[0] * WAVE + n], v1 = c_p * L.vals[slots[0] * WAVE + 32 + n];
+    const float bt0 = h ? -1.f : 2.f * v0, bt1 = h ? -1.f : 2.f * v1;
+    const float ct0 = -fmaf(v0, v0, 0.f), ct1 = -fmaf(v1, v1, 0.f);
+    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+      float s2[2] = {0.f, 0.f};
+      kde_mfma32_sums(kq32, ch * (cb >> 1), ch * (cb >> 1) + (cb >> 1), bt0, bt1, ct0, ct1, lane, s2);
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2[0]), __float_as_uint(s2[1]), false, false);
+      const float cs = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+      L.scr[ch * WAVE + lane] = cs;
+      tot += (double)cs;
+    }
+  } else {
+    KdeOps o;
+    kde_operands(L, slots, scl, nf, o);
+    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+      float s[4] = {0.f, 0.f, 0.f, 0.f};
+      kde_sums(kq, ch * cb, ch * cb + cb, o, nf, lane, s);
+      const float cs = kde_reduce_tiles(s, lane);
+      L.scr[ch * WAVE + lane] = cs;
+      tot += (double)cs;
+    }
   }
   float xv[4] = {0.f, 0.f, 0.f, 0.f};
   const float negsq = kde_own(L, slots, scl, nf, xv);
+  const int nfr = k32 ? -1 : nf;                      // replica form of the pass-1 elements
   const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
   // per-point records, 4 weight-0 rows before the first point, >= 4 after the last
   const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
   float shift = 0.f;
   if (!(tot > 0.0)) {                                 // every weight underflowed (or NaN parent)
     float amax = -INFINITY;
-    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nf));
+    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nfr));
     shift = amax;
     tot = 0.0;
     for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
       const int j0 = min(M, ch * cb * 16), j1 = min(M, j0 + cb * 16);
       float cs = 0.f;
       for (int j = j0; j < j1; ++j)
-        cs += __builtin_amdgcn_exp2f(kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nf) - shift);
+        cs += __builtin_amdgcn_exp2f(kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nfr) - shift);
       L.scr[ch * WAVE + lane] = cs;
       tot += (double)cs;
     }
@@ -1072,7 +1117,7 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int u = back ? 3 - v : v;
-      const float d = kde_arg_rec(r[u], xb0, xb1, xb2, negsq, nf);
+      const float d = kde_arg_rec(r[u], xb0, xb1, xb2, negsq, nfr);
       const int jj = j + u;
       const bool inside = back ? jj >= j0 : jj < j1;
       cs += inside ? __builtin_amdgcn_exp2f(d - shift) : 0.f;
@@ -1886,11 +1931,14 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   const int64_t per_wave = vbn_hip_lds_bytes(a->n_slots, a->max_out);
   const bool stage = staged_kinds(km);
   const int64_t wbuf_bytes = stage ? 2 * (int64_t)a->wbuf_floats * (int64_t)sizeof(float) : 0;
+  // small launches (e.g. Gibbs: one wave per 8 chains) keep >= 2 workgroups per CU first
+  const int64_t waves = (a->n_queries * (int64_t)a->n_samples + WAVE - 1) / WAVE;
   int nw = 0;
   int64_t lds = 0, best = 0;
   for (int w = stage ? WG_MAX_WAVES : 1; w >= 1; w >>= 1) {
     const int64_t l = w * per_wave + wbuf_bytes;
     if (l > 160 * 1024) continue;
+    if (w > 1 && waves / w < 2 * 256) continue;
     const int64_t res = std::min<int64_t>(16, (160 * 1024 / l) * w);
     if (res > best) { best = res; nw = w; lds = l; }
   }

@@ -38,7 +38,7 @@ STEP_INTS = 32
 (S_KIND, S_ROLE, S_FLAGS, S_ACT, S_NIN, S_INOFF, S_OUTCOL, S_OUTDIM, S_FIXEDCOL, S_K, S_NOUT,
  S_NODEID, S_NOISE, S_AUX0, S_AUX1, S_AUX2, S_OFF_STD, S_OFF_W1, S_OFF_W2, S_OFF_B2, S_OFF_W3,
  S_OFF_B3, S_OFF_TAIL, S_OFF_PTS, S_OFF_W2H, S_OFF_KQ, S_OFF_KQY, S_OFF_KR, S_OFF_KV,
- S_WBLK_OFF, S_WBLK_LEN) = range(31)
+ S_WBLK_OFF, S_WBLK_LEN, S_OFF_KQ32) = range(32)
 WBLK_CHUNK = 256          # floats per LDS-DMA wave instruction (64 lanes x 16 B)
 KDE_CHUNKS = 16
 MLP_HIDDEN = (32, 32)
@@ -110,6 +110,22 @@ def _kde_pack(feats: List[np.ndarray], records: bool = False) -> np.ndarray:
     if nf <= 2:
         a[:, nf + 1] = 1.0
     return a.reshape(rows // 16, 16, 4).transpose(0, 2, 1)
+
+
+def _kde_pack32(y: np.ndarray) -> np.ndarray:
+    """One-feature point pack of the 32x32x2 pass (csrc kde_mfma32_sums): per 32-point block
+    [y'_0..y'_31 | |y'|^2_0..|y'|^2_31]; the same points, |y'|^2 and padding (1e30) as
+    _kde_pack, so the chunk boundaries (multiples of 64 points) coincide."""
+    y = y.reshape(y.shape[0], -1).astype(np.float32)
+    m, nf = y.shape
+    if nf != 1:
+        raise ValueError("the 32x32x2 pack is for one-feature nodes")
+    rows = KDE_CHUNKS * _kde_cb(m) * 16
+    a = np.zeros((rows, 2), np.float32)
+    a[:, 1] = 1e30
+    a[:m, 0] = y[:, 0]
+    a[:m, 1] = (y.astype(np.float64) ** 2).sum(axis=1).astype(np.float32)
+    return a.reshape(rows // 32, 32, 2).transpose(0, 2, 1)
 
 
 def _kde_pack_valu(y: np.ndarray) -> np.ndarray:
@@ -267,6 +283,8 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
             offs["kq"] = blob.add(_kde_pack([_np(pts_p) * c_p]))
             offs["kr"] = blob.add(_kde_pack([_np(pts_p) * c_p], records=True))
             offs["kv"] = blob.add(_kde_pack_valu(_np(pts_p) * c_p))
+            if dp == 1:
+                offs["kq32"] = blob.add(_kde_pack32(_np(pts_p) * c_p))
         if dp + D <= 3:
             offs["kqy"] = blob.add(_kde_pack(([_np(pts_p) * c_p] if dp else []) + [_np(pts_y) * c_y]))
         stride = dp + D
@@ -494,6 +512,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         row[S_OFF_KQY] = npk.offs.get("kqy", -1)
         row[S_OFF_KR] = npk.offs.get("kr", -1)
         row[S_OFF_KV] = npk.offs.get("kv", -1)
+        row[S_OFF_KQ32] = npk.offs.get("kq32", -1)
         if "wblk" in npk.offs and (n in latent_s or n in logp_s or n in params_s):
             row[S_WBLK_OFF] = npk.offs["wblk"]
             row[S_WBLK_LEN] = npk.offs["wblk_len"]
