@@ -33,6 +33,7 @@
 
 #define WAVE 64
 #define KDE_CHUNKS 16
+#define KDE_REC_TAIL 8   // weight-0 record rows after the last point (plan.py KDE_REC_TAIL)
 #define LOG_2PI_F 1.8378770664093453f
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -931,7 +932,12 @@ __device__ __forceinline__ float kde_own(const Lane& L, const int (&slots)[4], c
 // (y'_0 .. y'_{nf-1}, |y'|^2, ..) of the per-point record pack.
 __device__ __forceinline__ float kde_arg_rec(const float4 r, float xb0, float xb1, float xb2, float negsq,
                                              int nf) {
-  if (nf < 0) return fmaf(r.y, -1.f, fmaf(r.x, xb0, negsq));   // one-feature 32x32x2 chain from C
+  if (nf < 0) {                       // "C form" of -nf features (32x32x2 MFMA, VALU pass 1)
+    float d = fmaf(r.x, xb0, negsq);
+    if (nf < -1) d = fmaf(r.y, xb1, d);
+    if (nf < -2) d = fmaf(r.z, xb2, d);
+    return fmaf(nf == -1 ? r.y : (nf == -2 ? r.z : r.w), -1.f, d);
+  }
   const bool zc = nf <= 2;
   float d = zc ? 0.f : negsq;
   d = fmaf(r.x, xb0, d);
@@ -999,9 +1005,6 @@ __device__ __forceinline__ void kde_sums(const float* __restrict__ kq, int b0, i
   else kde_mfma_sums<false>(kq, b0, b1, o, lane, s);
 }
 
-// Latent non-root KDE node, parent dims 1..3: index ~ softmax_j log K_p (kde.py:172-178).
-// Pass 1 (MFMA): per-chunk weight sums -> scr[chunk][lane]; pass 2 (VALU replica): locate the
-// chunk holding u * total, scan it.  All-underflow particles (every weight 0) redo the sums on
 // One-feature nodes: pass-1 sums on v_mfma_f32_32x32x2_f32 (1024 pairs per instruction, half
 // the matrix-pipe time of the 16x16x4 form): rows = 32 points (A = (y', |y'|^2), pack kq32
 // [block32][2][32]), columns = the 32 particles of tile t (B = (2x', -1)), C = -|x'|^2, i.e.
@@ -1014,20 +1017,75 @@ __device__ __forceinline__ void kde_mfma32_sums(const float* __restrict__ kq32, 
 #pragma unroll
   for (int r = 0; r < 16; ++r) { c0[r] = ct0; c1[r] = ct1; }
   f32x2 acc0 = f32x2{0.f, 0.f}, acc1 = f32x2{0.f, 0.f};
-  for (int b = b0; b < b1; ++b) {
-    const float a = kq32[b * 64 + lane];
-    const f32x16 d0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt0, c0, 0, 0, 0);
-    const f32x16 d1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt1, c1, 0, 0, 0);
+  // software pipeline: the exps of one MFMA run while the next MFMA is in the matrix pipe,
+  // the point operand two blocks ahead is in flight
+  if (b1 <= b0) return;
+  const float* __restrict__ pa = kq32 + b0 * 64 + lane;
+  const int nb = b1 - b0;
+  float an = pa[nb > 1 ? 64 : 0];
+  f32x16 q = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[0], bt1, c1, 0, 0, 0);
+  f32x16 d = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[0], bt0, c0, 0, 0, 0);
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      acc0 += f32x2{__builtin_amdgcn_exp2f(d0[r]), __builtin_amdgcn_exp2f(d0[r + 1])};
-      acc1 += f32x2{__builtin_amdgcn_exp2f(d1[r]), __builtin_amdgcn_exp2f(d1[r + 1])};
-    }
+  for (int r = 0; r < 16; r += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[r]), __builtin_amdgcn_exp2f(d[r + 1])};
+  for (int i = 1; i < nb; ++i) {
+    const float a = an;
+    an = pa[min(i + 1, nb - 1) * 64];
+    __builtin_amdgcn_sched_barrier(0);
+    d = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt0, c0, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[r]), __builtin_amdgcn_exp2f(q[r + 1])};
+    __builtin_amdgcn_sched_barrier(0);
+    q = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt1, c1, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[r]), __builtin_amdgcn_exp2f(d[r + 1])};
   }
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[r]), __builtin_amdgcn_exp2f(q[r + 1])};
   s[0] += acc0.x + acc0.y;
   s[1] += acc1.x + acc1.y;
 }
 
+// Inverse-CDF scan of one chunk [j0, j1) (pass 2).  A lane whose threshold lies in the upper
+// half of its chunk scans backwards from the end for the right-hand mass csum - rem: the
+// point found is the same (the largest j with cum(j-1) <= rem), and no lane scans more than
+// about half a chunk.  Backward lanes walk the reversed record copy forward, so every lane
+// reads 4 consecutive records per trip with the next 4 in flight and no per-lane selects.
+// The weights are summed in scan order (bit-identical running sums to a point-by-point
+// scan); a crossing past the chunk end (rounding) is clamped to the chunk's last point.
+// rec: records (plan.py _kde_pack records=True), rev = reversed copy; M points.
+template <class ARG>
+__device__ __forceinline__ int kde_scan(const float4* __restrict__ rec, const float4* __restrict__ rev, int M,
+                                        int j0, int j1, float rem, float csum, float shift, ARG arg) {
+  const bool back = rem > 0.5f * csum;
+  const float goal = back ? csum - rem : rem;
+  const float4* __restrict__ q = back ? rev + (M - j1) : rec + j0;
+  const int n = j1 - j0;
+  int kh = n - 1;
+  float cs = 0.f;
+  float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
+  for (int k = 0; k < n; k += 4) {
+    const float4 n0 = q[k + 4], n1 = q[k + 5], n2 = q[k + 6], n3 = q[k + 7];
+    const float c0 = cs + __builtin_amdgcn_exp2f(arg(r0) - shift);
+    const float c1 = c0 + __builtin_amdgcn_exp2f(arg(r1) - shift);
+    const float c2 = c1 + __builtin_amdgcn_exp2f(arg(r2) - shift);
+    const float c3 = c2 + __builtin_amdgcn_exp2f(arg(r3) - shift);
+    if (back ? c3 >= goal : c3 > goal) {
+      const int v = (back ? c0 >= goal : c0 > goal) ? 0
+                  : ((back ? c1 >= goal : c1 > goal) ? 1 : ((back ? c2 >= goal : c2 > goal) ? 2 : 3));
+      kh = min(k + v, n - 1);
+      break;
+    }
+    cs = c3;
+    r0 = n0; r1 = n1; r2 = n2; r3 = n3;
+  }
+  return min(max(back ? j1 - 1 - kh : j0 + kh, 0), M - 1);
+}
+
+// Latent non-root KDE node, parent dims 1..3: index ~ softmax_j log K_p (kde.py:172-178).
+// Pass 1 (MFMA): per-chunk weight sums -> scr[chunk][lane]; pass 2 (VALU replica): locate the
+// chunk holding u * total, scan it.  All-underflow particles (every weight 0) redo the sums on
 // VALU relative to their largest weight.
 __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
                                               float ucat, float c_p) {
@@ -1039,6 +1097,13 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   for (int f = 0; f < nf; ++f) slots[f] = L.ic[st.in_off + f];
   const bool k32 = nf == 1 && st.reserved[7] >= 0;   // one-feature node with the 32x32x2 pack
   double tot = 0.0;
+  float xv[4] = {0.f, 0.f, 0.f, 0.f};
+  const float negsq = kde_own(L, slots, scl, nf, xv);
+#ifdef VBN_ABL_NOP1
+  if (true) {
+    for (int ch = 0; ch < KDE_CHUNKS; ++ch) { L.scr[ch * WAVE + lane] = 1.f; tot += 1.0; }
+  } else
+#endif
   if (k32) {
     const float* __restrict__ kq32 = L.P + st.reserved[7];
     const int h = lane >> 5, n = lane & 31;
@@ -1064,11 +1129,9 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
       tot += (double)cs;
     }
   }
-  float xv[4] = {0.f, 0.f, 0.f, 0.f};
-  const float negsq = kde_own(L, slots, scl, nf, xv);
   const int nfr = k32 ? -1 : nf;                      // replica form of the pass-1 elements
   const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
-  // per-point records, 4 weight-0 rows before the first point, >= 4 after the last
+  // per-point records (4 weight-0 rows before the first point), then the reversed copy
   const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
   float shift = 0.f;
   if (!(tot > 0.0)) {                                 // every weight underflowed (or NaN parent)
@@ -1094,39 +1157,29 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
     cum = nx;
   }
   const int j0 = min(M, ch * cb * 16), j1 = min(M, j0 + cb * 16);
+#ifdef VBN_ABL_NOSCAN
+  wave_sync();
+  return min(j0, M - 1);
+#endif
   const float rem = (float)(thr - cum);
   const float csum = L.scr[ch * WAVE + lane];
-  // Scan the chunk over the records, 4 points per trip with the next 4 in flight.  A lane
-  // whose threshold lies in the upper half of its chunk scans backwards from the end for the
-  // right-hand mass csum - rem: the point found is the same (the largest j with
-  // cum(j-1) <= rem), and no lane scans more than about half a chunk.
-  const bool back = rem > 0.5f * csum;
-  const float goal = back ? csum - rem : rem;
-  const int step = back ? -4 : 4;
-  const int nb16 = ((M + 15) >> 4) * 16;           // records valid on [-4, nb16 + 4)
-  int j = back ? j1 - 4 : j0;                      // first record of the current trip
-  int idx = back ? j0 : max(j1 - 1, 0);
-  float cs = 0.f;
-  float4 r[4], rn[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) r[u] = rec[j + u];
-  for (int it = 0; it < (j1 - j0 + 3) / 4; ++it, j += step) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) rn[u] = rec[min(max(j + step, -4), nb16) + u];
-    int hit = -1;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int u = back ? 3 - v : v;
-      const float d = kde_arg_rec(r[u], xb0, xb1, xb2, negsq, nfr);
-      const int jj = j + u;
-      const bool inside = back ? jj >= j0 : jj < j1;
-      cs += inside ? __builtin_amdgcn_exp2f(d - shift) : 0.f;
-      if (hit < 0 && inside && (back ? cs >= goal : cs > goal)) hit = jj;
-    }
-    if (hit >= 0) { idx = hit; break; }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) r[u] = rn[u];
-  }
+  const float4* __restrict__ rev = rec + (((M + 15) >> 4) * 16 + KDE_REC_TAIL);
+  int idx;
+  // the replica chain per feature count, compile-time (kde_arg_rec)
+  if (nfr == -1)
+    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
+                   [&](const float4 r) { return fmaf(r.y, -1.f, fmaf(r.x, xb0, negsq)); });
+  else if (nfr == 1)
+    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
+                   [&](const float4 r) { return fmaf(1.f, negsq, fmaf(r.y, -1.f, fmaf(r.x, xb0, 0.f))); });
+  else if (nfr == 2)
+    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift, [&](const float4 r) {
+      return fmaf(1.f, negsq, fmaf(r.z, -1.f, fmaf(r.y, xb1, fmaf(r.x, xb0, 0.f))));
+    });
+  else
+    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift, [&](const float4 r) {
+      return fmaf(r.w, -1.f, fmaf(r.z, xb2, fmaf(r.y, xb1, fmaf(r.x, xb0, negsq))));
+    });
   wave_sync();
   return idx;
 }
@@ -1221,7 +1274,7 @@ __device__ __forceinline__ int kde_index_valu(const vbn_walk_args& A, const vbn_
     L.scr[ch * WAVE + lane] = cs;
     tot += (double)cs;
   }
-  // per-point records, 4 weight-0 rows before the first point, >= 4 after the last
+  // per-point records (4 weight-0 rows before the first point), then the reversed copy
   const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
   float shift = 0.f;
   if (!(tot > 0.0)) {                                 // every weight underflowed (or NaN parent)
@@ -1248,34 +1301,9 @@ __device__ __forceinline__ int kde_index_valu(const vbn_walk_args& A, const vbn_
   const int j0 = min(M, ch * csz), j1 = min(M, j0 + csz);
   const float rem = (float)(thr - cum);
   const float csum = L.scr[ch * WAVE + lane];
-  // bidirectional chunk scan (see kde_index_mfma)
-  const bool back = rem > 0.5f * csum;
-  const float goal = back ? csum - rem : rem;
-  const int step = back ? -4 : 4;
-  const int nb16 = ((M + 15) >> 4) * 16;           // records valid on [-4, nb16 + 4)
-  int j = back ? j1 - 4 : j0;
-  int idx = back ? j0 : max(j1 - 1, 0);
-  float cs = 0.f;
-  float4 r[4], rn[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) r[u] = rec[j + u];
-  for (int it = 0; it < (j1 - j0 + 3) / 4; ++it, j += step) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) rn[u] = rec[min(max(j + step, -4), nb16) + u];
-    int hit = -1;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int u = back ? 3 - v : v;
-      const float d = kde_arg_valu<NF>(xv, r[u]);
-      const int jj = j + u;
-      const bool inside = back ? jj >= j0 : jj < j1;
-      cs += inside ? __builtin_amdgcn_exp2f(d - shift) : 0.f;
-      if (hit < 0 && inside && (back ? cs >= goal : cs > goal)) hit = jj;
-    }
-    if (hit >= 0) { idx = hit; break; }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) r[u] = rn[u];
-  }
+  const float4* __restrict__ rev = rec + (((M + 15) >> 4) * 16 + KDE_REC_TAIL);
+  const int idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
+                           [&](const float4 r) { return kde_arg_valu<NF>(xv, r); });
   wave_sync();
   return idx;
 }

@@ -41,6 +41,7 @@ STEP_INTS = 32
  S_WBLK_OFF, S_WBLK_LEN, S_OFF_KQ32) = range(32)
 WBLK_CHUNK = 256          # floats per LDS-DMA wave instruction (64 lanes x 16 B)
 KDE_CHUNKS = 16
+KDE_REC_TAIL = 8       # weight-0 record rows after the last point (csrc kde_scan prefetch)
 MLP_HIDDEN = (32, 32)
 KDE_MAX_DIMS = 4
 MAX_NODES = 1 << 14
@@ -90,23 +91,26 @@ def _kde_pack(feats: List[np.ndarray], records: bool = False) -> np.ndarray:
     MFMA A-operand image: [KDE_CHUNKS * cb][4][16] fp32 (cb = _kde_cb(M) blocks per chunk),
     columns (y'_0 .. y'_{nf-1}, |y'|^2, 1) for nf <= 2 and (y'_0, y'_1, y'_2, |y'|^2) for
     nf == 3; padding points get |y'|^2 = 1e30, i.e. weight exp2(-1e30) = 0.
-    ``records=True``: per-point rows (y'.., |y'|^2) [4 + 16 ceil(M/16) + 4][4] with weight-0
-    rows before the first point and after the last (the inverse-CDF scan reads one trip of 4
-    past either end of a chunk).
+    ``records=True``: per-point rows (y'.., |y'|^2): [4 + 16 ceil(M/16) + 8][4] forward, then the
+    points in reverse order [16 ceil(M/16) + 8][4], weight-0 rows around them (the inverse-CDF
+    scan walks either array forward, two trips of 4 past a chunk end at most).
     """
     y = np.concatenate([f.reshape(f.shape[0], -1) for f in feats], axis=1).astype(np.float32)
     m, nf = y.shape
     if nf > 3:
         raise ValueError("kde MFMA pack supports at most 3 features")
     nblk = (m + 15) // 16
-    rows = 4 + nblk * 16 + 4 if records else KDE_CHUNKS * _kde_cb(m) * 16
+    rows = 4 + nblk * 16 + KDE_REC_TAIL if records else KDE_CHUNKS * _kde_cb(m) * 16
     a = np.zeros((rows, 4), np.float32)
     o = 4 if records else 0
     a[:, nf] = 1e30
     a[o:o + m, :nf] = y
     a[o:o + m, nf] = (y.astype(np.float64) ** 2).sum(axis=1).astype(np.float32)
     if records:
-        return a
+        rev = np.zeros((nblk * 16 + KDE_REC_TAIL, 4), np.float32)
+        rev[:, nf] = 1e30
+        rev[:m] = a[o:o + m][::-1]
+        return np.concatenate([a, rev])
     if nf <= 2:
         a[:, nf + 1] = 1.0
     return a.reshape(rows // 16, 16, 4).transpose(0, 2, 1)
