@@ -348,3 +348,23 @@ def test_kde_pack32_gives_kernel_weights():
     ref = np.exp(-0.5 * ((parts[:, None, 0].astype(np.float64) - pts[None, :, 0]) ** 2) / s ** 2)
     np.testing.assert_allclose(w[:, :m], ref, rtol=1e-5, atol=1e-30)
     assert (w[:, m:] == 0).all()
+
+
+def test_kde_records_carry_a_reversed_copy():
+    """Records pack (csrc kde_scan): [4 + nb16 + KDE_REC_TAIL] forward rows (weight-0 padding
+    around the points), then the points reversed in [nb16 + KDE_REC_TAIL] rows, so backward
+    scans walk forward and a trip of 4 plus its prefetch never leaves the array."""
+    from vectorizedbayesiannetwork_amd.plan import KDE_REC_TAIL, _kde_pack
+    rng = np.random.default_rng(3)
+    for m, nf in ((1, 1), (37, 2), (64, 3)):
+        y = rng.normal(size=(m, nf)).astype(np.float32)
+        r = _kde_pack([y], records=True)
+        nb16 = (m + 15) // 16 * 16
+        assert r.shape == (4 + nb16 + KDE_REC_TAIL + nb16 + KDE_REC_TAIL, 4)
+        fwd, rev = r[4:4 + m], r[4 + nb16 + KDE_REC_TAIL:]
+        np.testing.assert_array_equal(fwd[:, :nf], y)
+        np.testing.assert_array_equal(rev[:m], fwd[::-1])
+        pad = np.ones(len(r), bool)
+        pad[4:4 + m] = False
+        pad[4 + nb16 + KDE_REC_TAIL:4 + nb16 + KDE_REC_TAIL + m] = False
+        assert (r[pad, nf] == np.float32(1e30)).all()
