@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 5
+#define VBN_ABI_VERSION 6
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001
@@ -152,6 +152,10 @@ typedef struct vbn_walk_args {
   int32_t n_noise;         /* noise nodes per sweep (injected-noise stride, mode GIBBS) */
   int32_t wbuf_floats;     /* >= every step's wblk_len: size of each of the two LDS weight
                               buffers shared by the waves of a workgroup                */
+  int32_t wave_particles;  /* particles per wave64: 64 (0 = 64) or 32, the half-wave form for
+                              launches too small to fill the chip (Gibbs at a few thousand
+                              chains): lanes 32-63 mirror lanes 0-31 (same particle and draws,
+                              no writes) and the MLPs run one 32-particle MFMA group   */
 } vbn_walk_args;
 
 int vbn_hip_abi_version(void);

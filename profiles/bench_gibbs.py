@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--cpu-sweeps", type=int, default=4)
     ap.add_argument("--cpu-chains", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--wave-particles", type=int, default=None, help="32 / 64 (default: the engine's choice)")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     cfg, g, model, vbn, query = Bm.build_workload("cfg2", "cuda:0", 0)
@@ -63,7 +64,8 @@ def main():
     reps_ev = -(-B // cfg["B"])                      # more chains than cfg2 queries: tile the evidence rows
     query = {"target": query["target"],
              "evidence": {k: v.repeat(reps_ev, 1)[:B].contiguous() for k, v in query["evidence"].items()}}
-    vbn.set_sampling_method("gibbs", n_samples=args.n_samples, burn_in=args.burn_in, n_steps=args.thin, seed=1)
+    vbn.set_sampling_method("gibbs", n_samples=args.n_samples, burn_in=args.burn_in, n_steps=args.thin, seed=1,
+                            wave_particles=args.wave_particles)
     for _ in range(args.warmup):
         vbn.sample(query, n_samples=args.n_samples)
     torch.cuda.synchronize()
@@ -84,11 +86,12 @@ def main():
     fx = E._fixed_buffer(gp.init, vals, B, pk.device)
     state = torch.randn(gp.init.n_slots + 1, B * 8, device=pk.device)
     from vectorizedbayesiannetwork_amd import ops
+    wp = eng._wave_particles(B)
 
     def launch(seed):
         return ops.gibbs_walk(gp.steps, gp.in_cols, pk.params, fx, None, state, B, gp.init.n_slots,
                               gp.init.max_out, gp.init.fixed_ld, B, gp.n_noise, pk.dmax, 1, iters, iters - 1, 1,
-                              0, seed, 1, gp.kind_mask)
+                              0, seed, 1, gp.kind_mask, gp.wbuf, wp)
     launch(0)
     stream = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -112,7 +115,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (cfg2 DAG/SEM/query generator; random-init CPD weights)",
         "config": {"workload": "gibbs32: 32node-gaussian_nn-gibbs", "chains": B, "n_samples": args.n_samples,
-                   "burn_in": args.burn_in, "n_steps": args.thin, "sweeps": iters, "candidates": 8},
+                   "burn_in": args.burn_in, "n_steps": args.thin, "sweeps": iters, "candidates": 8,
+                   "wave_particles": wp},
         "roofline": {"bound": "mfma", "achieved": round(ach, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
                      "frac": round(ach / peak, 4), "traffic": None, "kernel": "vbn_walk_kernel (GIBBS)",
                      "kernel_ms": round(kern_ms, 3), "flops_per_launch": f32 + hid,

@@ -85,3 +85,29 @@ def test_gibbs_production_rng_chain_and_reference_modes():
     assert x0.shape == (B, 1, 1)
     with pytest.raises(ValueError, match="collect"):
         GibbsSampler(collect="bogus")
+
+
+@pytest.mark.parametrize("kinds", [("gaussian_nn",), ("gaussian_nn", "linear_gaussian", "mdn", "kde", "softmax_nn")])
+def test_gibbs_half_wave_launch_matches_full_wave(kinds):
+    """wave_particles 32 (lanes 32-63 mirror 0-31, one MFMA group, include/vbn_hip.h) gives the
+    full-wave launch's chains: same Philox draws per (chain, candidate, sweep), same values; a
+    chain count that is not a multiple of 4 leaves a partial last wave."""
+    from vectorizedbayesiannetwork_amd import VBN, synthetic
+    from vectorizedbayesiannetwork_amd.engines import GibbsSampler
+    from vectorizedbayesiannetwork_amd.model import random_init_model
+    g = synthetic.random_dag(12, seed=0)
+    data = synthetic.sem_data(g, 512, seed=0)
+    model = random_init_model(g, synthetic.round_robin_kinds(g, kinds), data, seed=0,
+                              overrides={"kde": {"max_points": 256}})
+    vbn = VBN.from_model(model, device="cuda")
+    target, ev_nodes = synthetic.default_query_nodes(g, seed=1)
+    B = 301
+    torch.manual_seed(0)
+    ev = {n: data[n][:B].reshape(B, 1).clone() for n in ev_nodes}
+    q = vbn._normalize_query({"target": target, "evidence": ev})
+    outs = [GibbsSampler(n_samples=6, burn_in=3, n_steps=2, collect="chain", seed=11, wave_particles=wp).sample(vbn, q)
+            for wp in (64, 32)]
+    assert outs[0].shape == (B, 6, 1) and torch.isfinite(outs[0]).all()
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=1e-5)
+    with pytest.raises(ValueError, match="wave_particles"):
+        GibbsSampler(wave_particles=16)

@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -62,6 +62,7 @@ class VbnWalkArgs(ctypes.Structure):
         ("gibbs_thin", ctypes.c_int32),
         ("n_noise", ctypes.c_int32),
         ("wbuf_floats", ctypes.c_int32),
+        ("wave_particles", ctypes.c_int32),
     ]
 
 

@@ -117,6 +117,7 @@ struct Lane {
   int s;         // sample (Gibbs: candidate)
   int iter;      // Gibbs sweep (0 for every other walk)
   bool valid;    // particle index inside the batch
+  bool mirror;   // half-wave launch: lanes 32-63 mirror lanes 0-31 (wave-uniform)
 };
 
 // Draws of node ``st``, dimension d, for this particle.  Stream 0 gives a standard normal
@@ -458,7 +459,9 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
   }
   if (!exact) {
     float y[16];
-    if (mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 1, y, [] {})) {
+    if (L.mirror) {
+      h1 = h0;                                    // group 1 = group 0's particles
+    } else if (mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 1, y, [] {})) {
       exact = true;
     } else {
       const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
@@ -471,8 +474,12 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
     float y[16];
     mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 0, y, [] {});
     h0 = layer2_exact(st, L, 0, y);
-    mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 1, y, [] {});
-    h1 = layer2_exact(st, L, 1, y);
+    if (L.mirror) {
+      h1 = h0;
+    } else {
+      mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 1, y, [] {});
+      h1 = layer2_exact(st, L, 1, y);
+    }
   }
   mlp_head<ACT>(st, L, W, h0, h1, nan_in);
 }
@@ -1482,7 +1489,7 @@ __device__ __forceinline__ void gibbs_select(const vbn_walk_args& A, const vbn_s
 
 __device__ __forceinline__ void gibbs_collect(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
   const int it = L.iter, burn = A.gibbs_burn_in, thin = max(A.gibbs_thin, 1);
-  if (it < burn || (it - burn) % thin != 0 || L.s != 0 || !L.valid) return;     // 83-87
+  if (it < burn || (it - burn) % thin != 0 || L.s != 0 || !L.valid || (L.mirror && L.lane >= 32)) return;  // 83-87
   const int n_collect = (A.gibbs_iters - burn + thin - 1) / thin;
   const int k = (it - burn) / thin;
   for (int d = 0; d < st.out_dim; ++d)
@@ -1585,7 +1592,11 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
   L.scr = L.vals + A.n_slots * WAVE;
   L.wb = wbuf;
   const int64_t total = A.n_queries * (int64_t)A.n_samples;
-  const int64_t p_raw = ((int64_t)blockIdx.x * nw + wave) * WAVE + L.lane;
+  // half-wave launches (wave_particles 32): lane l and l + 32 carry the same particle, so
+  // every draw and value agrees; only the lower half writes, the MLPs run group 0 only
+  L.mirror = A.wave_particles == 32;
+  const int wp = L.mirror ? 32 : WAVE;
+  const int64_t p_raw = ((int64_t)blockIdx.x * nw + wave) * wp + (L.lane & (wp - 1));
   const bool valid = p_raw < total;
   L.p = valid ? p_raw : total - 1;
   L.b = L.p / A.n_samples;
@@ -1626,7 +1637,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
     }
   }
   }
-  if (!valid) return;
+  if (!valid || (L.mirror && L.lane >= 32)) return;
   if (A.mode == VBN_MODE_GIBBS) return;                  // outputs written by COLLECT steps
   if (A.state && (A.state_flags & 2)) {
     for (int c = 0; c < A.n_slots; ++c) A.state[(int64_t)c * total + L.p] = vread(L, c);
@@ -1943,6 +1954,9 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
     return fail(VBN_E_ARGS, "vbn_hip_walk: out_x without out_cols");
   if (a->wbuf_floats < 0 || (a->wbuf_floats % WBLK_CHUNK) != 0)
     return fail(VBN_E_ARGS, "vbn_hip_walk: wbuf_floats must be a non-negative multiple of 256");
+  if (a->wave_particles != 0 && a->wave_particles != 32 && a->wave_particles != WAVE)
+    return fail(VBN_E_ARGS, "vbn_hip_walk: wave_particles must be 0, 32 or 64");
+  const int64_t wp = a->wave_particles == 32 ? 32 : WAVE;   // particles per wave
   // smallest instantiated kind set covering the plan
   static const unsigned masks[] = {1u, 2u, 3u, 4u, 8u, 16u, 20u, 23u, 31u, 63u};
   const unsigned want = (unsigned)a->kind_mask & 63u;
@@ -1960,7 +1974,7 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   const bool stage = staged_kinds(km);
   const int64_t wbuf_bytes = stage ? 2 * (int64_t)a->wbuf_floats * (int64_t)sizeof(float) : 0;
   // small launches (e.g. Gibbs: one wave per 8 chains) keep >= 2 workgroups per CU first
-  const int64_t waves = (a->n_queries * (int64_t)a->n_samples + WAVE - 1) / WAVE;
+  const int64_t waves = (a->n_queries * (int64_t)a->n_samples + wp - 1) / wp;
   int nw = 0;
   int64_t lds = 0, best = 0;
   for (int w = stage ? WG_MAX_WAVES : 1; w >= 1; w >>= 1) {
@@ -1976,7 +1990,7 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
        a->gibbs_thin <= 0 || !a->out_x || (a->noise && a->n_noise <= 0)))
     return fail(VBN_E_ARGS, "vbn_hip_walk: Gibbs walk needs 8 candidates, iters > burn_in >= 0, thin > 0, out_x");
   const int64_t total = a->n_queries * (int64_t)a->n_samples;
-  const int64_t blocks = (total + (int64_t)WAVE * nw - 1) / ((int64_t)WAVE * nw);
+  const int64_t blocks = (total + wp * nw - 1) / (wp * nw);
   if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
   const dim3 grid((unsigned)blocks), block(WAVE * nw);
   hipStream_t st = (hipStream_t)stream;

@@ -578,15 +578,27 @@ class GibbsSampler(_EngineBase):
     at every collected sweep instead (burn-in, thinning by ``n_steps``) -- the Markov chain.
     """
 
+    # below this many candidate lanes (B x 8) the sweep launch runs half-wave (4 chains per
+    # wave64, include/vbn_hip.h wave_particles): 1536 full waves = 1.5 per SIMD
+    HALF_WAVE_BELOW = 1536 * 64
+
     def __init__(self, n_samples: int = 200, burn_in: int = 10, n_steps: int = 1, collect: str = "reference",
-                 **kwargs):
+                 wave_particles: Optional[int] = None, **kwargs):
         super().__init__(n_samples=n_samples, **kwargs)
+        if wave_particles not in (None, 32, 64):
+            raise ValueError(f"wave_particles must be None (auto), 32 or 64, got {wave_particles!r}")
+        self.wave_particles = wave_particles
         self.burn_in = int(burn_in)
         self.n_steps = int(n_steps)
         self.n_candidates = 8
         if collect not in ("reference", "chain"):
             raise ValueError(f"collect must be 'reference' or 'chain', got {collect!r}")
         self.collect = collect
+
+    def _wave_particles(self, b: int) -> int:
+        if self.wave_particles is not None:
+            return self.wave_particles
+        return 32 if b * 8 < self.HALF_WAVE_BELOW else 64
 
     def _gibbs_plan(self, pk: PackedModel, target: str, vals) -> GibbsPlan:
         model = pk.model
@@ -642,7 +654,7 @@ class GibbsSampler(_EngineBase):
         out = ops.gibbs_walk(gp.steps, gp.in_cols, pk.params, fx,
                              sweep_noise, chains.contiguous(), b, init.n_slots, init.max_out, init.fixed_ld,
                              noise_b, gp.n_noise, pk.dmax, dt, iters, burn, th, self.q_base, seed, 1,
-                             gp.kind_mask, gp.wbuf)
+                             gp.kind_mask, gp.wbuf, self._wave_particles(b))
         if self.collect == "chain" and n > 0:
             return out
         return out.expand(b, max(n, 1), dt).contiguous()

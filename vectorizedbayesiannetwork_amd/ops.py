@@ -156,9 +156,12 @@ def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samp
 def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: Optional[Tensor],
                state: Tensor, n_queries: int, n_slots: int, max_out: int, fixed_ld: int, noise_b: int,
                n_noise: int, dmax: int, out_dim: int, iters: int, burn_in: int, thin: int, q_base: int,
-               seed: int, offset: int, kind_mask: int, wbuf: int = 0) -> Tensor:
+               seed: int, offset: int, kind_mask: int, wbuf: int = 0, wave_particles: int = 64) -> Tensor:
     """``iters`` Gibbs sweeps (gibbs.py:34-87) over B chains x 8 candidate lanes, started from
-    ``state`` [n_slots + 1, B*8]; returns the collected target values [B, n_collect, out_dim]."""
+    ``state`` [n_slots + 1, B*8]; returns the collected target values [B, n_collect, out_dim].
+    ``wave_particles`` 32: half-wave launch (4 chains per wave64, include/vbn_hip.h)."""
+    if wave_particles not in (32, 64):
+        raise ValueError(f"vbn_hip::gibbs_walk: wave_particles must be 32 or 64, got {wave_particles}")
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::gibbs_walk runs on the GPU only (no CPU fallback); "
@@ -214,6 +217,7 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
     a.gibbs_thin = thin
     a.n_noise = n_noise
     a.wbuf_floats = int(wbuf)
+    a.wave_particles = int(wave_particles)
     lib = _lib.load()
     with torch.cuda.device(device):
         _lib.check(lib.vbn_hip_walk(ctypes.byref(a), ctypes.c_void_p(_stream_handle(device))), "vbn_hip_walk")
@@ -222,7 +226,8 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
 
 @gibbs_walk.register_fake
 def _gibbs_walk_fake(steps, in_cols, params, fixed, noise, state, n_queries, n_slots, max_out, fixed_ld,
-                     noise_b, n_noise, dmax, out_dim, iters, burn_in, thin, q_base, seed, offset, kind_mask, wbuf=0):
+                     noise_b, n_noise, dmax, out_dim, iters, burn_in, thin, q_base, seed, offset, kind_mask, wbuf=0,
+                     wave_particles=64):
     return params.new_empty((n_queries, (iters - burn_in + thin - 1) // thin, out_dim))
 
 
