@@ -1,1655 +1,13 @@
-// vbn_walk.hip — gfx950 (MI355X) particle walk for batched Bayesian-network inference.
-//
-// One wave64 owns 64 particles (lane == particle in every per-particle stage).  The wave
-// walks the plan's topological steps; each node's value lives in LDS (vals[slot][64]), so
-// the [B,S,sum(D)] particle tensor of the reference never touches HBM: only evidence in,
-// pdf/log-weights and the target slice out.
-//
-// NN CPDs (gaussian_nn, mdn, softmax_nn; MLP in->32->32->out): the 32x32 hidden layer runs
-// on MFMA (v_mfma_f32_32x32x2_f32, exact f32) with the hidden unit on the M axis and the
-// particle on the N axis, two 32-particle groups per wave.  Layer 1 (K = #parents <= few)
-// is computed on VALU directly in the MFMA B-operand layout, the head on VALU from the
-// accumulator layout, combined across lane halves with one v_permlane32_swap per output.
-//
-// Reference ops replaced (file:line in Giovannibriglia/VectorizedBayesianNetwork):
-//   topo loop            vbn/inference/monte_carlo_marginalization.py:60-91,
-//                        importance_sampling.py:56-80, likelihood_weighting.py:41-71,
-//                        vbn/sampling/ancestral.py:26-40
-//   gaussian_nn          vbn/cpds/gaussian_nn.py:215-288
-//   linear_gaussian      vbn/cpds/linear_gaussian.py:163-217
-//   mdn                  vbn/cpds/mdn.py:185-272
-//   kde                  vbn/cpds/kde.py:105-182
-//   softmax_nn           vbn/cpds/softmax_nn.py:581-759
-//   softmax + ESS        importance_sampling.py:82-84, likelihood_weighting.py:75-80
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include <math.h>
-#include <stdio.h>
-#include <string.h>
-
-#include <algorithm>
-
-#include "vbn_hip.h"
-
-#define WAVE 64
-#define KDE_CHUNKS 16
-#define KDE_REC_TAIL 8   // weight-0 record rows after the last point (plan.py KDE_REC_TAIL)
-#define LOG_2PI_F 1.8378770664093453f
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// step field holding the split-f16 W2 fragments (vbn_step.reserved[0])
-#define OFF_W2H(st) ((st).reserved[0])
-
-// ------------------------------------------------------------------------------------------
-// small device helpers
-// ------------------------------------------------------------------------------------------
-
-__device__ __forceinline__ void wave_sync() {
-  // LDS ops of one wave are issued in order; this only stops the compiler from moving
-  // LDS accesses of different lanes across the hand-off point.
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __builtin_amdgcn_wave_barrier();
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-// relu as one v_max_i32 on the float's bits (negative floats are negative ints; -0 -> +0).
-// fmaxf would add a canonicalising v_max(x, x) in IEEE mode, inline asm would hide the
-// MFMA->VALU read hazard from the compiler.  NaN parents are handled by the caller.
-__device__ __forceinline__ float relu_nan(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
-
-template <int ACT>
-__device__ __forceinline__ float act_fn(float x) {
-  if (ACT == VBN_ACT_RELU) return relu_nan(x);
-  if (ACT == VBN_ACT_TANH) return tanhf(x);
-  if (ACT == VBN_ACT_GELU) return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
-  return x > 0.f ? x : expm1f(x);  // ELU(alpha=1)
-}
-
-// F.softplus(beta=1, threshold=20) (reference cpds/utils.py:6-7) with hardware exp/log:
-// log1p(e) as Kahan's log(u) * e / (u - 1) (u - 1 is exact) for x >= -5, a 4-term series
-// below (relative error < 1e-9 there).
-__device__ __forceinline__ float softplus_t(float x) {
-#ifdef VBN_ABL_NOSOFTPLUS
-  return x;
-#endif
-  if (x > 20.f) return x;
-  const float e = __expf(x);
-  if (x < -5.f) return e * (1.f - e * (0.5f - e * (0.33333334f - e * 0.25f)));
-  const float u = 1.0f + e;
-  return __logf(u) * __fdividef(e, u - 1.0f);
-}
-
-// Philox-2x32-10 counter-based RNG (Random123): counter (c0, c1), 32-bit key; one
-// v_mad_u64_u32 per round.
-__device__ __forceinline__ uint2 philox2x32(uint2 c, uint32_t k) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    const uint64_t p = (uint64_t)0xD256D193u * c.x;
-    c = make_uint2((uint32_t)(p >> 32) ^ k ^ c.y, (uint32_t)p);
-    k += 0x9E3779B9u;
-  }
-  return c;
-}
-
-__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
-
-__device__ __forceinline__ float box_muller(uint32_t a, uint32_t b) {
-  const float u1 = (float)((a >> 8) + 1u) * (1.0f / 16777216.0f);  // (0,1]
-  const float u2 = (float)(b >> 8) * (1.0f / 16777216.0f);
-  const float r = __builtin_sqrtf(-2.0f * __logf(u1));
-  return r * __builtin_amdgcn_cosf(u2);                              // cos(2*pi*u2)
-}
-
-struct Lane {
-  const float* P;        // parameter blob (from a __restrict__ kernel argument)
-  const int32_t* ic;     // parent column slots (from a __restrict__ kernel argument)
-  float* vals;   // LDS [n_slots][64]
-  float* scr;    // LDS [max_out][64]
-  const float* wb;  // LDS: this step's weight block (wblk, staged one step ahead by the workgroup)
-  int lane;
-  int64_t p;     // particle (clamped)
-  int64_t b;     // query (Gibbs: chain)
-  int s;         // sample (Gibbs: candidate)
-  int iter;      // Gibbs sweep (0 for every other walk)
-  bool valid;    // particle index inside the batch
-  bool mirror;   // half-wave launch: lanes 32-63 mirror lanes 0-31 (wave-uniform)
-};
-
-// Draws of node ``st``, dimension d, for this particle.  Stream 0 gives a standard normal
-// (Box-Muller on both words), stream 1 two uniforms: the categorical / index choice and the
-// within-bin uniform, stream 2 the Gibbs chain choice (one per chain and sweep).  Counter =
-// (sample, query ^ seed_hi), key = seed_lo + stream id, where the query key is 0 for draws
-// shared by all queries (root nodes in MCM/LW/ancestral, Q5).  Stream id = offset[8] |
-// node[14] | dim[8] | stream[2]: disjoint for every (node, dim, stream) the host admits
-// (PackedModel: < 16384 nodes, < 256 dims per node).
-// With injected noise (parity tests) slot 0 = categorical uniform, slot 1 = normal / uniform.
-#define RNG_NORMAL 0
-#define RNG_UNIFORM 1
-#define RNG_SELECT 2
-__device__ __forceinline__ uint2 rng_words(const vbn_walk_args& A, const vbn_step& st, int d, int stream,
-                                           const Lane& L) {
-  const uint32_t qkey = (st.flags & VBN_F_SHARED) ? 0u : (uint32_t)(A.q_base + L.b + 1);
-  const uint32_t sid = ((uint32_t)(A.offset & 0xffu) << 24) | ((uint32_t)st.node_id << 10) |
-                       ((uint32_t)d << 2) | (uint32_t)stream;
-  const uint32_t ctr = (uint32_t)L.s + (uint32_t)L.iter * (uint32_t)A.n_samples;
-  return philox2x32(make_uint2(ctr, qkey ^ (uint32_t)(A.seed >> 32)), (uint32_t)A.seed + sid);
-}
-
-__device__ __forceinline__ int64_t noise_index(const vbn_walk_args& A, const vbn_step& st, int d, int slot,
-                                               const Lane& L) {
-  const int64_t bq = A.noise_b == 1 ? 0 : L.b;
-  const int64_t stride_slot = (int64_t)A.noise_b * A.n_samples * A.dmax;
-  const int64_t stride_iter = (int64_t)A.n_noise * 2 * stride_slot;       // Gibbs sweeps
-  return (int64_t)L.iter * stride_iter + ((int64_t)st.noise_idx * 2 + slot) * stride_slot +
-         (bq * A.n_samples + L.s) * A.dmax + d;
-}
-
-__device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
-  if (A.noise) return A.noise[noise_index(A, st, d, 1, L)];
-#ifdef VBN_ABL_NORNG
-  return 0.5f;
-#endif
-  const uint2 w = rng_words(A, st, d, RNG_NORMAL, L);
-  return box_muller(w.x, w.y);
-}
-
-// (categorical uniform, within-bin uniform)
-__device__ __forceinline__ float2 draw_uniforms(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
-  if (A.noise) return make_float2(A.noise[noise_index(A, st, d, 0, L)], A.noise[noise_index(A, st, d, 1, L)]);
-  const uint2 w = rng_words(A, st, d, RNG_UNIFORM, L);
-  return make_float2(u01(w.x), u01(w.y));
-}
-
-__device__ __forceinline__ float vread(const Lane& L, int slot) { return L.vals[slot * WAVE + L.lane]; }
-__device__ __forceinline__ void vwrite(const Lane& L, int slot, float v) { L.vals[slot * WAVE + L.lane] = v; }
-
-__device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_step& st, int d,
-                                             const Lane& L) {
-  const int64_t row = A.fixed_per_particle ? L.p : L.b;
-  return A.fixed[row * A.fixed_ld + st.fixed_col + d];
-}
-
-// value of a fixed node: from the fixed buffer, or (VBN_F_KEEP, Gibbs) the slot's current value
-__device__ __forceinline__ float node_fixed(const vbn_walk_args& A, const vbn_step& st, int d,
-                                            const Lane& L) {
-  return (st.flags & VBN_F_KEEP) ? vread(L, st.out_col + d) : fixed_value(A, st, d, L);
-}
-
-// ------------------------------------------------------------------------------------------
-// MLP (in -> 32 -> 32 -> n_out) for the wave's 64 particles; head outputs to scr[j][lane].
-//
-// Two 32-particle groups per wave (g = 0: particles 0-31, g = 1: 32-63).  Both hidden layers
-// run with the hidden unit on M and the particle on N; both accumulators start from the layer's
-// bias (register r of lane half h = b[row(r, h)], four 16-byte loads, exact f32).
-//   layer 1: K = n_in on v_mfma_f32_32x32x2_f32, A = W1 fragments, B = z of the lane's particle
-//   layer 2: K = 32 on v_mfma_f32_32x32x16_f16 as a 3-pass split product: x = hi + lo with
-//            hi = f16(x), lo = f16(x - hi) for both operands; A_lo.B_hi + A_hi.B_lo + A_hi.B_hi
-//            accumulated in f32 (relative error ~2^-22 per product, i.e. fp32-level) at 1/5
-//            of the f32-MFMA time.  The layer-1 accumulator IS the B operand: register 8s+j
-//            of lane half h holds hidden row 16s + 8(j>>2) + 4h + (j&3), and the host packs
-//            W2 in that k order.  If any |h| > 32768 (f16 range) the wave takes the exact
-//            f32 chain (v_mfma_f32_32x32x2_f32, k-step s pairs rows (row(s,0), row(s,1))).
-//   head   : 16 v_permlane32_swap transpose the layer-2 accumulators so lane l holds all 32
-//            hidden units of particle l; the head then runs on VALU with wave-uniform weights.
-//
-// Parameter blocks (packed by vectorizedbayesiannetwork_amd/plan.py):
-//   off_std : mean_x[n_in], 1/std_x[n_in]                            (gaussian_nn only)
-//   off_w1  : [t][64]  lane l: W1z[l&31][2t + (l>>5)],  W1z = [W1 | 0] (even width)
-//   off_b2  : [layer 2][group 2][half 2][16] = b[row(r, h)] (accumulator init; the two group
-//             copies are identical)
-//   off_w2  : [q 4][lane 64][4], step s = 4q+e: W2[l&31][row(s, l>>5)]   (exact f32 fallback)
-//   off_w2h : [4][lane 64][8 f16]: hi(s=0), hi(s=1), lo(s=0), lo(s=1);
-//             element j of lane l: W2[l&31][16s + 8(j>>2) + 4(l>>5) + (j&3)]
-//   off_w3  : [n_out][32] = W3[j][row(r,0)] (r<16) ++ W3[j][row(r,1)]
-//   off_b3  : [n_out]
-// with row(r, h) = (r&3) + 8(r>>2) + 4h, the 32x32 accumulator row of register r, half h.
-// ------------------------------------------------------------------------------------------
-
-// layer-1 B operand of k-step t for group g: z[2t + half] of particle (c + 32 g); the
-// column beyond n_in (odd n_in) is 0.
-template <bool STD, int NIN>
-__device__ __forceinline__ float l1_operand(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
-                                            int t, int g) {
-  const float* __restrict__ P = L.P;
-  const int half = L.lane >> 5;
-  const int nin = NIN > 0 ? NIN : st.n_in;
-  const int kk = 2 * t + half;
-  const int ke = min(2 * t, nin - 1), ko = min(2 * t + 1, nin - 1);
-  const int slot = half ? L.ic[st.in_off + ko] : L.ic[st.in_off + ke];
-  float z = L.vals[slot * WAVE + (L.lane & 31) + 32 * g];
-  if (STD) {
-    const float m = half ? P[st.off_std + ko] : P[st.off_std + ke];
-    const float is = half ? P[st.off_std + nin + ko] : P[st.off_std + nin + ke];
-    z = (z - m) * is;
-  }
-  return kk < nin ? z : 0.0f;
-}
-
-#define WBLK_OFF(st) ((st).reserved[5])
-#define WBLK_LEN(st) ((st).reserved[6])
-
-// Layer-1 accumulator init of group g = bias rows of the lane half (register r of half h =
-// b1[row(r, h)]), from the staged weight block (LDS) or, on the exact fallback, the blob.
-__device__ __forceinline__ f32x16 load_acc16(const float* __restrict__ src) {
-  const float4* q4 = reinterpret_cast<const float4*>(src);
-  f32x16 a;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 v = q4[q];
-    a[4 * q] = v.x; a[4 * q + 1] = v.y; a[4 * q + 2] = v.z; a[4 * q + 3] = v.w;
-  }
-  return a;
-}
-
-// layer-2 bias as the accumulator's initial value of group g (exact f32 fallback path)
-__device__ __forceinline__ f32x16 layer2_init(const vbn_step& st, const Lane& L, int g) {
-  const float4* bacc = reinterpret_cast<const float4*>(L.P + st.off_b2 + 64 + 32 * g + 16 * (L.lane >> 5));
-  f32x16 b;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 v = bacc[q];
-    b[4 * q] = v.x; b[4 * q + 1] = v.y; b[4 * q + 2] = v.z; b[4 * q + 3] = v.w;
-  }
-  return b;
-}
-
-// y - f32(half h of packed f16 pair hp), exact: one v_fma_mix_f32 (reads the f16 in place).
-// Operands are VALU results (activation / cvt), never raw MFMA results, so no MFMA read hazard.
-__device__ __forceinline__ float sub_f16_lo(float y, uint32_t hp) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(y));
-  return r;
-}
-__device__ __forceinline__ float sub_f16_hi(float y, uint32_t hp) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(y));
-  return r;
-}
-
-// Layer 2 of one group on the split-f16 path from the activations y (|y| <= 32768 checked by
-// the caller): y = hi + lo with hi = f16(y), lo = f16(y - hi); A_lo.B_hi + A_hi.B_lo + A_hi.B_hi
-// on v_mfma_f32_32x32x16_f16 (f32 accumulate).  B operand: register 8s+j of lane half h holds
-// hidden row 16s + 8(j>>2) + 4h + (j&3).
-__device__ __forceinline__ f32x16 layer2_split(const uint4 (&w2h)[4], const f32x16& binit, const float (&y)[16]) {
-#ifdef VBN_ABL_NOL2
-  f32x16 r = binit;
-  for (int i = 0; i < 16; ++i) r[i] += y[i];
-  return r;
-#endif
-  f16x8 bh[2], bl[2];
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const float y0 = y[8 * s2 + j], y1 = y[8 * s2 + j + 1];
-      const f16x2 ph = __builtin_convertvector((f32x2){y0, y1}, f16x2);
-      const uint32_t hp = __builtin_bit_cast(uint32_t, ph);
-#ifdef VBN_ABL_NOSPLIT
-      const f16x2 pl = ph;
-#else
-      const f16x2 pl = __builtin_convertvector((f32x2){sub_f16_lo(y0, hp), sub_f16_hi(y1, hp)}, f16x2);
-#endif
-      bh[s2][j] = ph[0];
-      bh[s2][j + 1] = ph[1];
-      bl[s2][j] = pl[0];
-      bl[s2][j + 1] = pl[1];
-    }
-  }
-  f32x16 b = binit;
-#pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2) {
-    const f16x8 ah = __builtin_bit_cast(f16x8, w2h[s2]);
-    const f16x8 al = __builtin_bit_cast(f16x8, w2h[2 + s2]);
-#ifndef VBN_ABL_NOSPLIT
-    b = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s2], b, 0, 0, 0);
-    b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s2], b, 0, 0, 0);
-#endif
-    b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s2], b, 0, 0, 0);
-  }
-  return b;
-}
-
-// Layer 2 of one group from the activations y, exact f32 chain (K = 32 as 16
-// v_mfma_f32_32x32x2_f32 steps)
-__device__ __forceinline__ f32x16 layer2_exact(const vbn_step& st, const Lane& L, int g, const float (&y)[16]) {
-  const float4* w2p = reinterpret_cast<const float4*>(L.P + st.off_w2);
-  f32x16 b = layer2_init(st, L, g);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4 v = w2p[q * WAVE + L.lane];
-    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, y[4 * q + 0], b, 0, 0, 0);
-    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, y[4 * q + 1], b, 0, 0, 0);
-    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, y[4 * q + 2], b, 0, 0, 0);
-    b = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, y[4 * q + 3], b, 0, 0, 0);
-  }
-  return b;
-}
-
-// Head outputs two at a time (both outputs' weights in flight together; w3/b3 (weight block)
-// and scr (head scratch) are distinct LDS rows, so the reads need not wait for the writes).
-__device__ __forceinline__ float head_dot(const float4 (&w)[4], const float (&y0)[16], const float (&y1)[16],
-                                          float b, bool nan_in) {
-  float a0 = 0.f, c0 = 0.f, a1 = 0.f, c1 = 0.f;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    a0 = fmaf(w[q].x, y0[4 * q], a0);
-    c0 = fmaf(w[q].y, y0[4 * q + 1], c0);
-    a1 = fmaf(w[q].x, y1[4 * q], a1);
-    c1 = fmaf(w[q].y, y1[4 * q + 1], c1);
-    a0 = fmaf(w[q].z, y0[4 * q + 2], a0);
-    c0 = fmaf(w[q].w, y0[4 * q + 3], c0);
-    a1 = fmaf(w[q].z, y1[4 * q + 2], a1);
-    c1 = fmaf(w[q].w, y1[4 * q + 3], c1);
-  }
-  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0 + c0), __float_as_uint(a1 + c1), false, false);
-  const float o = (__uint_as_float(sw[0]) + __uint_as_float(sw[1])) + b;
-  return nan_in ? __int_as_float(0x7fc00000) : o;
-}
-
-__device__ __forceinline__ void head_outputs(const float* __restrict__ w3, const float* __restrict__ b3,
-                                             float* __restrict__ scr, int nout, const float (&y0)[16],
-                                             const float (&y1)[16], bool nan_in) {
-#pragma clang loop unroll(disable)
-  for (int j = 0; j < nout; j += 2) {
-    const bool two = j + 1 < nout;
-    const float4* wa = reinterpret_cast<const float4*>(w3 + 32 * j);
-    const float4* wb = reinterpret_cast<const float4*>(w3 + 32 * (two ? j + 1 : j));
-    const float4 va[4] = {wa[0], wa[1], wa[2], wa[3]};
-    const float4 vb[4] = {wb[0], wb[1], wb[2], wb[3]};
-    const float ba = b3[j], bb = b3[two ? j + 1 : j];
-    scr[j * WAVE] = head_dot(va, y0, y1, ba, nan_in);
-    if (two) scr[(j + 1) * WAVE] = head_dot(vb, y0, y1, bb, nan_in);
-  }
-}
-
-// Head on VALU in the accumulator layout (no transpose): lane half h holds hidden rows
-// row(r, h) of its particle, so per output j the half's 16 products use per-lane weights
-// W3[j][row(r, h)] (the pack's [n_out][32] rows hold 16 per half), in two independent chains
-// per group; one v_permlane32_swap per output then adds the two halves (group 0 | group 1 ->
-// lane l = particle l).  W = the step's weight block (W3 at off_w3, b3 at off_b3, relative to
-// wblk_off); outputs to scr[j][lane].
-template <int ACT>
-__device__ __forceinline__ void mlp_head(const vbn_step& st, const Lane& L, const float* __restrict__ W,
-                                         const f32x16& h0, const f32x16& h1, bool nan_in) {
-  const int lane = L.lane;
-#ifdef VBN_ABL_NOHEAD
-  for (int j = 0; j < st.n_out; ++j) L.scr[j * WAVE + lane] = h0[j] + h1[j + 1];
-  wave_sync();
-  return;
-#endif
-  float y0[16], y1[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    y0[r] = act_fn<ACT>(h0[r]);
-    y1[r] = act_fn<ACT>(h1[r]);
-  }
-  head_outputs(W + (st.off_w3 - WBLK_OFF(st)) + 16 * (lane >> 5), W + (st.off_b3 - WBLK_OFF(st)),
-               L.scr + lane, st.n_out, y0, y1, nan_in);
-  wave_sync();
-}
-
-// Layer 1 of group g (v_mfma_f32_32x32x2_f32, K = n_in, bias rows as the accumulator init)
-// and its activation.  W = weight block base (LDS: staged block; global: blob + wblk_off), so
-// W1 sits at W[t * 64 + lane] and the biases at W + (off_b2 - wblk_off).  ``pre`` runs between
-// the fragment reads and the first MFMA (group 0: the step's draws).  Returns true
-// (wave-uniform) when some activation leaves the f16 split range |y| <= 32768 (NaN with the
-// sign bit clear counts as out of range).
-template <int ACT, bool STD, int NIN, typename F>
-__device__ __forceinline__ bool mlp_l1_act(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
-                                           const float* __restrict__ W, int g, float (&y)[16], F&& pre) {
-  const int lane = L.lane;
-  f32x16 a = load_acc16(W + (st.off_b2 - WBLK_OFF(st)) + 32 * g + 16 * (lane >> 5));
-  if (NIN > 0) {
-    float w1[(NIN + 1) / 2 > 0 ? (NIN + 1) / 2 : 1];
-#pragma unroll
-    for (int t = 0; t < (NIN + 1) / 2; ++t) w1[t] = W[t * WAVE + lane];
-    pre();
-#pragma unroll
-    for (int t = 0; t < (NIN + 1) / 2; ++t)
-      a = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[t], l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
-  } else {
-    pre();
-    const int t1 = (st.n_in + 1) >> 1;
-    for (int t = 0; t < t1; ++t)
-      a = __builtin_amdgcn_mfma_f32_32x32x2f32(W[t * WAVE + lane], l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
-  }
-  int big = 0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    y[r] = act_fn<ACT>(a[r]);
-    big = max(big, __float_as_int(y[r]));        // activations are >= -1: only the positive side
-  }
-  return __any(big > 0x47000000);
-}
-
-// One NN node for the wave's 64 particles from the LDS-staged weight block: group 0 (layer 1,
-// range check, layer 2 split-f16 on MFMA), then group 1, the head on both.  ``pre`` (the
-// step's draws, independent of the MLP) runs after group 0's fragment reads are issued.  An
-// f16-range miss in either group, or VBN_F_F32L2, sends both groups to the exact f32 chain
-// (layer 1 recomputed there from the blob).
-template <int ACT, bool STD, int NIN, typename F>
-__device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
-  const int lane = L.lane;
-  const int nin = NIN > 0 ? NIN : st.n_in;
-  const float* __restrict__ W = L.wb;
-  const uint4* w2h = reinterpret_cast<const uint4*>(W + (OFF_W2H(st) - WBLK_OFF(st)));
-  const float* b2 = W + (st.off_b2 - WBLK_OFF(st)) + 64 + 16 * (lane >> 5);
-  bool nan_in = false;                            // torch keeps NaN through Linear/act
-  for (int d = 0; d < nin; ++d) {
-    const float v = L.vals[L.ic[st.in_off + d] * WAVE + lane];
-    nan_in |= (v != v);
-  }
-  f32x16 h0, h1;
-  bool exact = (st.flags & VBN_F_F32L2) != 0;
-  bool pre_done = false;
-  if (!exact) {
-    float y[16];
-    pre_done = true;
-    if (mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 0, y, pre)) {
-      exact = true;
-    } else {
-      const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
-      h0 = layer2_split(wq, load_acc16(b2), y);
-    }
-  }
-  if (!exact) {
-    float y[16];
-    if (L.mirror) {
-      h1 = h0;                                    // group 1 = group 0's particles
-    } else if (mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 1, y, [] {})) {
-      exact = true;
-    } else {
-      const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
-      h1 = layer2_split(wq, load_acc16(b2 + 32), y);
-    }
-  }
-  if (exact) {
-    if (!pre_done) pre();
-    const float* __restrict__ Wg = L.P + WBLK_OFF(st);
-    float y[16];
-    mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 0, y, [] {});
-    h0 = layer2_exact(st, L, 0, y);
-    if (L.mirror) {
-      h1 = h0;
-    } else {
-      mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 1, y, [] {});
-      h1 = layer2_exact(st, L, 1, y);
-    }
-  }
-  mlp_head<ACT>(st, L, W, h0, h1, nan_in);
-}
-
-template <int ACT, bool STD, typename F>
-__device__ __forceinline__ void mlp_nin(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
-  switch (st.n_in) {
-    case 1: mlp_forward<ACT, STD, 1>(A, st, L, pre); break;
-    case 2: mlp_forward<ACT, STD, 2>(A, st, L, pre); break;
-    case 3: mlp_forward<ACT, STD, 3>(A, st, L, pre); break;
-    default: mlp_forward<ACT, STD, 0>(A, st, L, pre); break;
-  }
-}
-
-// KM bit 5: some NN CPD uses a non-relu activation.  ``pre``: the step's draws (see mlp_forward).
-template <unsigned KM, typename F>
-__device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
-  const bool sd = (st.flags & VBN_F_STANDARDIZE) != 0;
-  if (!(KM & 32) || st.act == VBN_ACT_RELU) {
-    if (sd) mlp_nin<VBN_ACT_RELU, true>(A, st, L, pre); else mlp_nin<VBN_ACT_RELU, false>(A, st, L, pre);
-    return;
-  }
-  if constexpr ((KM & 32) != 0) {
-    switch (st.act * 2 + (sd ? 1 : 0)) {
-      case 2: mlp_nin<VBN_ACT_TANH, false>(A, st, L, pre); break;
-      case 3: mlp_nin<VBN_ACT_TANH, true>(A, st, L, pre); break;
-      case 4: mlp_nin<VBN_ACT_GELU, false>(A, st, L, pre); break;
-      case 5: mlp_nin<VBN_ACT_GELU, true>(A, st, L, pre); break;
-      case 6: mlp_nin<VBN_ACT_ELU, false>(A, st, L, pre); break;
-      default: mlp_nin<VBN_ACT_ELU, true>(A, st, L, pre); break;
-    }
-  }
-}
-
-// value of node dim d for this particle: fresh draw result or fixed input
-#define NODE_X(d) (vread(L, st.out_col + (d)))
-
-// ------------------------------------------------------------------------------------------
-// gaussian_nn (gaussian_nn.py:215-288)
-//   tail (non-root): std_y[D], mean_y[D], min_scale
-//   tail (root)    : loc[D], scale[D], log_scale[D]
-// ------------------------------------------------------------------------------------------
-template <unsigned KM>
-__device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
-#pragma clang fp contract(off)
-  const float* __restrict__ P = L.P;
-  const int D = st.out_dim;
-  const bool latent = st.role == VBN_ROLE_LATENT;
-  const bool want_lp = (st.flags & VBN_F_LOGP) != 0;
-  const float* t = P + st.off_tail;
-  if (st.flags & VBN_F_ROOT) {
-    for (int d = 0; d < D; ++d) {
-      const float loc = t[d], scale = t[D + d];
-      if (st.role == VBN_ROLE_PARAMS) {
-        vwrite(L, st.out_col + d, loc);
-        vwrite(L, st.out_col + D + d, scale);
-        continue;
-      }
-      float x;
-      if (latent) {
-        x = draw_normal(A, st, d, L) * scale + loc;  // torch.normal(loc, scale)
-        vwrite(L, st.out_col + d, x);
-      } else {
-        x = node_fixed(A, st, d, L);
-        vwrite(L, st.out_col + d, x);
-      }
-      if (want_lp) {                                 // Normal.log_prob (gaussian_nn.py:276-279)
-        const float diff = x - loc;
-        lp += -(diff * diff) / (2.0f * (scale * scale)) - t[2 * D + d] - 0.91893853320467274178f;
-      }
-    }
-    return;
-  }
-  float eps0 = 0.f;                                 // dim-0 draw, issued beside the weight loads
-#ifdef VBN_LATE_DRAW
-  run_mlp<KM>(A, st, L, [] {});
-  if (latent) eps0 = draw_normal(A, st, 0, L);
-#else
-  run_mlp<KM>(A, st, L, [&]() { if (latent) eps0 = draw_normal(A, st, 0, L); });
-#endif
-  const float min_scale = t[2 * D];
-  float acc = 0.f;
-  for (int d = 0; d < D; ++d) {
-    const float o_loc = L.scr[d * WAVE + L.lane];
-    const float o_sc = L.scr[(D + d) * WAVE + L.lane];
-    const float sy = t[d], my = t[D + d];
-    const float loc = o_loc * sy + my;
-    const float scale = (softplus_t(o_sc) + min_scale) * sy;
-    if (st.role == VBN_ROLE_PARAMS) {
-      vwrite(L, st.out_col + d, loc);
-      vwrite(L, st.out_col + D + d, scale);
-      continue;
-    }
-    float x;
-    if (latent) {
-      x = loc + (d == 0 ? eps0 : draw_normal(A, st, d, L)) * scale;
-    } else {
-      x = node_fixed(A, st, d, L);
-    }
-    vwrite(L, st.out_col + d, x);
-    if (want_lp) {
-      const float diff = x - loc;
-      acc += (diff * diff) / (scale * scale) + 2.0f * __logf(scale) + LOG_2PI_F;
-    }
-  }
-  if (want_lp) lp += -0.5f * acc;
-}
-
-// ------------------------------------------------------------------------------------------
-// linear_gaussian (linear_gaussian.py:163-217)
-//   tail: W[D][n_in] (W[:, d] of the reference's [n_in, D]), bias[D], scale[D], log_scale[D]
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void step_linear_gaussian(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
-#pragma clang fp contract(off)
-  const float* __restrict__ P = L.P;
-  const int D = st.out_dim, nin = st.n_in;
-  const float* t = P + st.off_tail;
-  const float* W = t;
-  const float* bias = t + D * nin;
-  const float* scale = bias + D;
-  const float* log_scale = scale + D;
-  const bool latent = st.role == VBN_ROLE_LATENT;
-  float acc = 0.f;
-  for (int d = 0; d < D; ++d) {
-    float mu = 0.f;
-    for (int i = 0; i < nin; ++i) mu = fmaf(vread(L, L.ic[st.in_off + i]), W[d * nin + i], mu);
-    const float loc = (nin > 0) ? mu + bias[d] : bias[d];
-    if (st.role == VBN_ROLE_PARAMS) {
-      vwrite(L, st.out_col + d, loc);
-      vwrite(L, st.out_col + D + d, scale[d]);
-      continue;
-    }
-    float x;
-    if (latent) {
-      x = loc + draw_normal(A, st, d, L) * scale[d];
-    } else {
-      x = node_fixed(A, st, d, L);
-    }
-    vwrite(L, st.out_col + d, x);
-    if (st.flags & VBN_F_LOGP) {
-      const float diff = x - loc;
-      acc += (diff * diff) / (scale[d] * scale[d]) + 2.0f * log_scale[d] + LOG_2PI_F;
-    }
-  }
-  if (st.flags & VBN_F_LOGP) lp += -0.5f * acc;
-}
-
-// ------------------------------------------------------------------------------------------
-// categorical inverse-CDF: smallest k with cumsum(p)[k] > u * sum(p)
-// ------------------------------------------------------------------------------------------
-template <typename F>
-__device__ __forceinline__ int inv_cdf(int K, float u, F prob) {
-  float tot = 0.f;
-  for (int k = 0; k < K; ++k) tot += prob(k);
-  const float thr = u * tot;
-  float cum = 0.f;
-  int idx = K - 1;
-  for (int k = 0; k < K - 1; ++k) {
-    cum += prob(k);
-    if (cum > thr) { idx = k; break; }
-  }
-  return idx;
-}
-
-// ------------------------------------------------------------------------------------------
-// mdn (mdn.py:185-272)
-//   non-root: scr = [logits K][comp k: loc D, raw_scale D];  tail: min_scale
-//   root    : tail = pi[K], log_pi[K], loc[K*D], scale[K*D], log_scale[K*D], var[K*D]
-// ------------------------------------------------------------------------------------------
-template <unsigned KM>
-__device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
-#pragma clang fp contract(off)
-  const float* __restrict__ P = L.P;
-  const int D = st.out_dim, K = st.k;
-  const float* t = P + st.off_tail;
-  const bool root = (st.flags & VBN_F_ROOT) != 0;
-  const bool latent = st.role == VBN_ROLE_LATENT;
-  const bool want_lp = (st.flags & VBN_F_LOGP) != 0;
-  const int lane = L.lane;
-  float* scr = L.scr;
-  float min_scale = 0.f, lmax = 0.f, lsum = 1.f, psum = 1.f;
-  float u0 = 0.f, eps0 = 0.f;                       // component choice + dim-0 normal
-  auto draws = [&]() {
-    if (latent) {
-      u0 = draw_uniforms(A, st, 0, L).x;
-      eps0 = draw_normal(A, st, 0, L);
-    }
-  };
-  if (root) draws();
-  if (!root) {
-    run_mlp<KM>(A, st, L, draws);
-    min_scale = t[0];
-    // pi = softmax(logits).clamp_min(1e-5); pi /= sum (mdn.py:227-228)
-    lmax = -INFINITY;
-    for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, scr[k * WAVE + lane]);
-    lsum = 0.f;
-    for (int k = 0; k < K; ++k) lsum += __expf(scr[k * WAVE + lane] - lmax);
-    psum = 0.f;
-    for (int k = 0; k < K; ++k) psum += fmaxf(__expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f);
-    psum = fmaxf(psum, 1e-12f);
-  }
-  auto pi_k = [&](int k) -> float {
-    if (root) return t[k];
-    return fmaxf(__expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f) / psum;
-  };
-  auto loc_kd = [&](int k, int d) -> float {
-    return root ? t[2 * K + k * D + d] : scr[(K + k * 2 * D + d) * WAVE + lane];
-  };
-  auto scale_kd = [&](int k, int d) -> float {
-    return root ? t[2 * K + K * D + k * D + d]
-                : softplus_t(scr[(K + k * 2 * D + D + d) * WAVE + lane]) + min_scale;
-  };
-  if (latent) {
-    const int idx = inv_cdf(K, u0, pi_k);
-    for (int d = 0; d < D; ++d)
-      vwrite(L, st.out_col + d, loc_kd(idx, d) + (d == 0 ? eps0 : draw_normal(A, st, d, L)) * scale_kd(idx, d));
-  } else {
-    for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, node_fixed(A, st, d, L));
-  }
-  if (want_lp) {
-    // logsumexp_k(log pi_k + log N_k(x))  (mdn.py:263-272), online form
-    float m = -INFINITY, se = 0.f;
-    for (int k = 0; k < K; ++k) {
-      float acc = 0.f;
-      for (int d = 0; d < D; ++d) {
-        const float x = NODE_X(d);
-        float ls, var;
-        if (root) {
-          ls = t[2 * K + 2 * K * D + k * D + d];
-          var = t[2 * K + 3 * K * D + k * D + d];
-        } else {
-          ls = __logf(scale_kd(k, d));
-          var = __expf(2.0f * ls);
-        }
-        const float diff = x - loc_kd(k, d);
-        acc += (diff * diff) / var + 2.0f * ls + LOG_2PI_F;
-      }
-      const float lpi = root ? t[K + k] : __logf(pi_k(k));
-      const float term = lpi + (-0.5f * acc);
-      if (term == -INFINITY) continue;
-      if (term > m) {
-        se = se * __expf(m - term) + 1.0f;
-        m = term;
-      } else {
-        se += __expf(term - m);
-      }
-    }
-    lp += (m == -INFINITY) ? m : m + __logf(se);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// softmax_nn (softmax_nn.py:581-759)
-//   scr (non-root) = logits[D][C];  root logits table at off_pts ([D][C], already log_softmax'd)
-//   tail: edges[D][C+1], sample_values[D][C], class_values[D][C], within_scale, min_bw, min_bw2
-//   aux0 = within-bin mode, aux1 = discrete-dim bit mask
-// ------------------------------------------------------------------------------------------
-template <unsigned KM>
-__device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
-#pragma clang fp contract(off)
-  const float* __restrict__ P = L.P;
-  const int D = st.out_dim, C = st.k;
-  const float* t = P + st.off_tail;
-  const float* edges = t;
-  const float* svals = t + D * (C + 1);
-  const float* cvals = svals + D * C;
-  const float wscale = cvals[D * C + 0];
-  const float min_bw = cvals[D * C + 1];
-  const float min_bw2 = cvals[D * C + 2];
-  const bool root = (st.flags & VBN_F_ROOT) != 0;
-  const bool latent = st.role == VBN_ROLE_LATENT;
-  const bool clip = (st.flags & VBN_F_CLIP) != 0;
-  const int mode = st.aux0;
-  const int lane = L.lane;
-  float2 uu0 = make_float2(0.f, 0.f);               // dim-0 uniforms
-  auto draws = [&]() { if (latent) uu0 = draw_uniforms(A, st, 0, L); };
-  if (root) draws(); else run_mlp<KM>(A, st, L, draws);
-  float lp_acc = 0.f;
-  for (int d = 0; d < D; ++d) {
-    auto logit = [&](int c) -> float {
-      return root ? P[st.off_pts + d * C + c] : L.scr[(d * C + c) * WAVE + lane];
-    };
-    float m = -INFINITY;
-    for (int c = 0; c < C; ++c) m = fmaxf(m, logit(c));
-    float se = 0.f;
-    for (int c = 0; c < C; ++c) se += __expf(logit(c) - m);
-    if (st.role == VBN_ROLE_PARAMS) {                   // softmax(logits) (RB target, D = 1)
-      for (int c = 0; c < C; ++c) vwrite(L, st.out_col + c, __expf(logit(c) - m) / se);
-      return;
-    }
-    const bool disc = (st.aux1 >> d) & 1;
-    const float* e = edges + d * (C + 1);
-    float x;
-    int idx;
-    if (latent) {
-      const float2 uu = d == 0 ? uu0 : draw_uniforms(A, st, d, L);
-      idx = inv_cdf(C, uu.x, [&](int c) { return __expf(logit(c) - m) / se; });
-      const float left = e[idx];
-      const float right = e[idx + 1 < C ? idx + 1 : C];
-      const float width = fmaxf(right - left, min_bw);
-      const float center = 0.5f * (left + right);
-      if (disc) {
-        x = svals[d * C + idx];
-      } else {
-        float cont;
-        if (mode == VBN_WITHIN_UNIFORM) {
-          cont = left + uu.y * width;
-        } else if (mode == VBN_WITHIN_TRIANGULAR) {
-          const float lv = left + width * sqrtf(fmaxf(uu.y * 0.5f, 0.0f));
-          const float rv = right - width * sqrtf(fmaxf((1.0f - uu.y) * 0.5f, 0.0f));
-          cont = uu.y < 0.5f ? lv : rv;
-        } else {
-          cont = center + draw_normal(A, st, d, L) * fmaxf(wscale * width, min_bw);
-        }
-        if (clip) cont = fminf(fmaxf(cont, left), right);
-        x = cont;
-      }
-    } else {
-      x = node_fixed(A, st, d, L);
-    }
-    vwrite(L, st.out_col + d, x);
-    if (st.flags & VBN_F_LOGP) {
-      // bin: count(x >= edges) - 1 clamped (bit-exact); discrete: first exact class match
-      int bin;
-      if (disc) {
-        bin = 0;
-        for (int c = C - 1; c >= 0; --c)
-          if (x == cvals[d * C + c]) bin = c;
-      } else {
-        int cnt = 0;
-        for (int c = 0; c <= C; ++c) cnt += (x >= e[c]) ? 1 : 0;
-        bin = min(max(cnt - 1, 0), C - 1);
-      }
-      const float log_bin = logit(bin) - m - __logf(se);
-      float lw = 0.f;
-      if (!disc) {
-        const float left = e[bin];
-        const float right = e[bin + 1 < C ? bin + 1 : C];
-        const float width = fmaxf(right - left, min_bw);
-        const float center = 0.5f * (left + right);
-        const float xu = clip ? fminf(fmaxf(x, left), right) : x;
-        const bool inside = (x >= left) && (x <= right);
-        if (mode == VBN_WITHIN_UNIFORM) {
-          lw = -logf(width);
-          if (!clip && !inside) lw = -INFINITY;
-        } else if (mode == VBN_WITHIN_TRIANGULAR) {
-          const float dl = fmaxf(width * (center - left), min_bw2);
-          const float dr = fmaxf(width * (right - center), min_bw2);
-          float pdf = (xu <= center) ? 2.0f * (xu - left) / dl : 2.0f * (right - xu) / dr;
-          pdf = fmaxf(pdf, 0.0f);
-          lw = logf(fmaxf(pdf, 1e-12f));
-          if (!clip && !inside) lw = -INFINITY;
-        } else {
-          const float sigma = fmaxf(wscale * width, min_bw);
-          const float diff = xu - center;
-          lw = -(diff * diff) / (2.0f * (sigma * sigma)) - logf(sigma) - 0.91893853320467274178f;
-        }
-      }
-      lp_acc += log_bin + lw;
-    }
-  }
-  if (st.flags & VBN_F_LOGP) lp += lp_acc;
-}
-
-// ------------------------------------------------------------------------------------------
-// kde (kde.py:105-182)
-//   points at off_pts: [M][stride] = parents[dp] ++ targets[D]
-//   tail: inv_sp, inv_sy, noise_scale, cy, log_n;  aux0 = dp, aux1 = stride
-// Weights are taken relative to the kernel's peak (exp(-q/2) <= 1); if every weight of a
-// particle underflows the pass is redone relative to the particle's nearest point.
-// ------------------------------------------------------------------------------------------
-// squared scaled distance to point ``pt`` over the parent dims.  DP >= 0: parent values in
-// registers (pv); DP < 0: generic count, parent values re-read from LDS.
-template <int DP>
-__device__ __forceinline__ float kde_qp(const float* __restrict__ pt, const float (&pv)[4], float inv,
-                                        int dp, const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
-  float q = 0.f;
-  if (DP >= 0) {
-#pragma unroll
-    for (int i = 0; i < (DP >= 0 ? DP : 0); ++i) {
-      const float df = (pv[i] - pt[i]) * inv;
-      q = fmaf(df, df, q);
-    }
-  } else {
-    for (int i = 0; i < dp; ++i) {
-      const float df = (vread(L, L.ic[st.in_off + i]) - pt[i]) * inv;
-      q = fmaf(df, df, q);
-    }
-  }
-  return q;
-}
-
-template <int DY>
-__device__ __forceinline__ float kde_qy(const float* __restrict__ pty, float x0, float inv, int D,
-                                        const vbn_step& st, const Lane& L) {
-  if (DY == 1) {
-    const float df = (x0 - pty[0]) * inv;
-    return df * df;
-  }
-  float q = 0.f;
-  for (int d = 0; d < D; ++d) {
-    const float df = (vread(L, st.out_col + d) - pty[d]) * inv;
-    q = fmaf(df, df, q);
-  }
-  return q;
-}
-
-// ---- pairwise kernel weights on MFMA ------------------------------------------------------
-// The kernel weight of particle n and stored point m is exp(-|x_n - y_m|^2 / (2 s^2)) =
-// exp2(-|x'_n - y'_m|^2) with x' = c x, y' = c y, c = sqrt(log2(e) / 2) / s, and
-//   -|x' - y'|^2 = sum_k (2 x'_k) y'_k - |y'|^2 - |x'|^2,
-// a contraction over K <= 4 features: one v_mfma_f32_16x16x4_f32 per 16 points x 16 particles
-// (A = point features, host-packed as [block][k][16]; B = particle features; see KdeOps for
-// the two operand forms).  Padding points have |y'|^2 = 1e30 -> weight 0.  The MFMA is a
-// k-ordered fmaf chain from C, so kde_arg_rec() reproduces any element bit-for-bit on VALU
-// (the inverse-CDF scan).  The wave's 64 particles are 4 tiles of 16 (tile t = particles
-// 16t .. 16t+15); D layout: lane l holds points 4(l>>4) .. +3 of the block for particle
-// 16t + (l&15).  Bound: v_exp_f32 issue (one exp per pair); MFMA pipe 32 cycles per 256 pairs.
-struct KdeOps {
-  float b[4];      // B operand of tile t (feature l>>4 of particle 16t + (l&15))
-  float negsq[4];  // -|x'|^2 of particle 16t + (l&15)
-};
-
-// Two operand forms, chosen by the feature count nf (host packs match, plan.py _kde_pack):
-//   nf <= 2 ("ZC"): K = nf + 2, A = (y'.., |y'|^2, 1), B = (2x'.., -1, -|x'|^2), C = 0
-//   nf == 3       : K = 4,      A = (y'.., |y'|^2),    B = (2x'.., -1),          C = -|x'|^2
-// features: nf (slot, scale) pairs; slot = LDS value column.
-__device__ __forceinline__ void kde_operands(const Lane& L, const int (&slots)[4], const float (&scl)[4],
-                                             int nf, KdeOps& o) {
-  const int g = L.lane >> 4, n = L.lane & 15;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    float sq = 0.f, mine = 0.f;
-    for (int f = 0; f < nf; ++f) {
-      const float v = scl[f] * L.vals[slots[f] * WAVE + 16 * t + n];
-      sq = fmaf(v, v, sq);
-      if (f == g) mine = 2.f * v;
-    }
-    o.b[t] = g < nf ? mine : (g == nf ? -1.f : ((g == nf + 1 && nf <= 2) ? -sq : 0.f));
-    o.negsq[t] = -sq;
-  }
-}
-
-// the lane's own particle: x'_k and -|x'|^2 exactly as kde_operands computes them
-__device__ __forceinline__ float kde_own(const Lane& L, const int (&slots)[4], const float (&scl)[4], int nf,
-                                         float (&xv)[4]) {
-  float sq = 0.f;
-  for (int f = 0; f < nf; ++f) {
-    const float v = scl[f] * vread(L, slots[f]);
-    xv[f] = v;
-    sq = fmaf(v, v, sq);
-  }
-  return -sq;
-}
-
-// VALU replica of one MFMA output element (k-ordered fmaf chain from C), point record r =
-// (y'_0 .. y'_{nf-1}, |y'|^2, ..) of the per-point record pack.
-__device__ __forceinline__ float kde_arg_rec(const float4 r, float xb0, float xb1, float xb2, float negsq,
-                                             int nf) {
-  if (nf < 0) {                       // "C form" of -nf features (32x32x2 MFMA, VALU pass 1)
-    float d = fmaf(r.x, xb0, negsq);
-    if (nf < -1) d = fmaf(r.y, xb1, d);
-    if (nf < -2) d = fmaf(r.z, xb2, d);
-    return fmaf(nf == -1 ? r.y : (nf == -2 ? r.z : r.w), -1.f, d);
-  }
-  const bool zc = nf <= 2;
-  float d = zc ? 0.f : negsq;
-  d = fmaf(r.x, xb0, d);
-  d = nf > 1 ? fmaf(r.y, xb1, d) : d;
-  d = nf > 2 ? fmaf(r.z, xb2, d) : d;
-  const float y2 = nf == 1 ? r.y : (nf == 2 ? r.z : r.w);
-  d = fmaf(y2, -1.f, d);
-  return zc ? fmaf(1.f, negsq, d) : d;
-}
-
-// Blocks per chunk: a multiple of 4 (the host pads the pack to KDE_CHUNKS * kde_cb(M) blocks).
-__device__ __forceinline__ int kde_cb(int M) {
-  const int nblk = (M + 15) >> 4;
-  return (((nblk + KDE_CHUNKS - 1) / KDE_CHUNKS) + 3) & ~3;
-}
-
-// Sum of the lane's 4 tile partials across the 4 lane groups: lane l receives the total of
-// particle l (tile l>>4, column l&15).  Three cross-lane moves.
-__device__ __forceinline__ float kde_reduce_tiles(const float (&s)[4], int lane) {
-  const int h = lane >> 5, b = (lane >> 4) & 1;
-  float k0 = h ? s[2] : s[0], k1 = h ? s[3] : s[1];
-  const float o0 = h ? s[0] : s[2], o1 = h ? s[1] : s[3];
-  k0 += __shfl_xor(o0, 32);
-  k1 += __shfl_xor(o1, 32);
-  const float k = b ? k1 : k0, o = b ? k0 : k1;
-  return k + __shfl_xor(o, 16);
-}
-
-// per-lane partial sums of exp2(arg) over 16-point blocks [b0, b1) of pack kq, b1 - b0 a
-// multiple of 4 (padding blocks have weight 0); sums in packed pairs (v_pk_add_f32)
-template <bool ZC>
-__device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int b0, int b1, const KdeOps& o,
-                                              int lane, float (&s)[4]) {
-  f32x4 cin[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-    cin[t] = ZC ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4{o.negsq[t], o.negsq[t], o.negsq[t], o.negsq[t]};
-  f32x2 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x2{0.f, 0.f};
-  for (int b = b0; b < b1; b += 4) {
-    float a[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] = kq[(b + u) * 64 + lane];   // four loads in flight
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      f32x4 d[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], o.b[t], cin[t], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const f32x2 e01 = f32x2{__builtin_amdgcn_exp2f(d[t][0]), __builtin_amdgcn_exp2f(d[t][1])};
-        const f32x2 e23 = f32x2{__builtin_amdgcn_exp2f(d[t][2]), __builtin_amdgcn_exp2f(d[t][3])};
-        acc[t] += e01 + e23;
-      }
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 4; ++t) s[t] += acc[t].x + acc[t].y;
-}
-
-__device__ __forceinline__ void kde_sums(const float* __restrict__ kq, int b0, int b1, const KdeOps& o, int nf,
-                                         int lane, float (&s)[4]) {
-  if (nf <= 2) kde_mfma_sums<true>(kq, b0, b1, o, lane, s);
-  else kde_mfma_sums<false>(kq, b0, b1, o, lane, s);
-}
-
-// One-feature nodes: pass-1 sums on v_mfma_f32_32x32x2_f32 (1024 pairs per instruction, half
-// the matrix-pipe time of the 16x16x4 form): rows = 32 points (A = (y', |y'|^2), pack kq32
-// [block32][2][32]), columns = the 32 particles of tile t (B = (2x', -1)), C = -|x'|^2, i.e.
-// d = fmaf(|y'|^2, -1, fmaf(y', 2x', -|x'|^2)) (kde_arg_rec with nf < 0 replicates it).  Lane
-// (h, n) sums the exps of rows row(r, h) for particle 32 t + n; the two halves of both tiles
-// are added with one v_permlane32_swap per chunk.
-__device__ __forceinline__ void kde_mfma32_sums(const float* __restrict__ kq32, int b0, int b1, float bt0, float bt1,
-                                                float ct0, float ct1, int lane, float (&s)[2]) {
-  f32x16 c0, c1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { c0[r] = ct0; c1[r] = ct1; }
-  f32x2 acc0 = f32x2{0.f, 0.f}, acc1 = f32x2{0.f, 0.f};
-  // software pipeline: the exps of one MFMA run while the next MFMA is in the matrix pipe,
-  // the point operand two blocks ahead is in flight
-  if (b1 <= b0) return;
-  const float* __restrict__ pa = kq32 + b0 * 64 + lane;
-  const int nb = b1 - b0;
-  float an = pa[nb > 1 ? 64 : 0];
-  f32x16 q = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[0], bt1, c1, 0, 0, 0);
-  f32x16 d = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[0], bt0, c0, 0, 0, 0);
-#pragma unroll
-  for (int r = 0; r < 16; r += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[r]), __builtin_amdgcn_exp2f(d[r + 1])};
-  for (int i = 1; i < nb; ++i) {
-    const float a = an;
-    an = pa[min(i + 1, nb - 1) * 64];
-    __builtin_amdgcn_sched_barrier(0);
-    d = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt0, c0, 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[r]), __builtin_amdgcn_exp2f(q[r + 1])};
-    __builtin_amdgcn_sched_barrier(0);
-    q = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt1, c1, 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[r]), __builtin_amdgcn_exp2f(d[r + 1])};
-  }
-#pragma unroll
-  for (int r = 0; r < 16; r += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[r]), __builtin_amdgcn_exp2f(q[r + 1])};
-  s[0] += acc0.x + acc0.y;
-  s[1] += acc1.x + acc1.y;
-}
-
-// Inverse-CDF scan of one chunk [j0, j1) (pass 2).  A lane whose threshold lies in the upper
-// half of its chunk scans backwards from the end for the right-hand mass csum - rem: the
-// point found is the same (the largest j with cum(j-1) <= rem), and no lane scans more than
-// about half a chunk.  Backward lanes walk the reversed record copy forward, so every lane
-// reads 4 consecutive records per trip with the next 4 in flight and no per-lane selects.
-// The weights are summed in scan order (bit-identical running sums to a point-by-point
-// scan); a crossing past the chunk end (rounding) is clamped to the chunk's last point.
-// rec: records (plan.py _kde_pack records=True), rev = reversed copy; M points.
-template <class ARG>
-__device__ __forceinline__ int kde_scan(const float4* __restrict__ rec, const float4* __restrict__ rev, int M,
-                                        int j0, int j1, float rem, float csum, float shift, ARG arg) {
-  const bool back = rem > 0.5f * csum;
-  const float goal = back ? csum - rem : rem;
-  const float4* __restrict__ q = back ? rev + (M - j1) : rec + j0;
-  const int n = j1 - j0;
-  int kh = n - 1;
-  float cs = 0.f;
-  float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
-  for (int k = 0; k < n; k += 4) {
-    const float4 n0 = q[k + 4], n1 = q[k + 5], n2 = q[k + 6], n3 = q[k + 7];
-    const float c0 = cs + __builtin_amdgcn_exp2f(arg(r0) - shift);
-    const float c1 = c0 + __builtin_amdgcn_exp2f(arg(r1) - shift);
-    const float c2 = c1 + __builtin_amdgcn_exp2f(arg(r2) - shift);
-    const float c3 = c2 + __builtin_amdgcn_exp2f(arg(r3) - shift);
-    if (back ? c3 >= goal : c3 > goal) {
-      const int v = (back ? c0 >= goal : c0 > goal) ? 0
-                  : ((back ? c1 >= goal : c1 > goal) ? 1 : ((back ? c2 >= goal : c2 > goal) ? 2 : 3));
-      kh = min(k + v, n - 1);
-      break;
-    }
-    cs = c3;
-    r0 = n0; r1 = n1; r2 = n2; r3 = n3;
-  }
-  return min(max(back ? j1 - 1 - kh : j0 + kh, 0), M - 1);
-}
-
-// Latent non-root KDE node, parent dims 1..3: index ~ softmax_j log K_p (kde.py:172-178).
-// Pass 1 (MFMA): per-chunk weight sums -> scr[chunk][lane]; pass 2 (VALU replica): locate the
-// chunk holding u * total, scan it.  All-underflow particles (every weight 0) redo the sums on
-// VALU relative to their largest weight.
-__device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
-                                              float ucat, float c_p) {
-  const float* __restrict__ kq = L.P + st.reserved[1];
-  const int M = st.k, nf = st.aux0, lane = L.lane;
-  const int cb = kde_cb(M);
-  int slots[4] = {0, 0, 0, 0};
-  float scl[4] = {c_p, c_p, c_p, c_p};
-  for (int f = 0; f < nf; ++f) slots[f] = L.ic[st.in_off + f];
-  const bool k32 = nf == 1 && st.reserved[7] >= 0;   // one-feature node with the 32x32x2 pack
-  double tot = 0.0;
-  float xv[4] = {0.f, 0.f, 0.f, 0.f};
-  const float negsq = kde_own(L, slots, scl, nf, xv);
-#ifdef VBN_ABL_NOP1
-  if (true) {
-    for (int ch = 0; ch < KDE_CHUNKS; ++ch) { L.scr[ch * WAVE + lane] = 1.f; tot += 1.0; }
-  } else
-#endif
-  if (k32) {
-    const float* __restrict__ kq32 = L.P + st.reserved[7];
-    const int h = lane >> 5, n = lane & 31;
-    const float v0 = c_p * L.vals[slots[0] * WAVE + n], v1 = c_p * L.vals[slots[0] * WAVE + 32 + n];
-    const float bt0 = h ? -1.f : 2.f * v0, bt1 = h ? -1.f : 2.f * v1;
-    const float ct0 = -fmaf(v0, v0, 0.f), ct1 = -fmaf(v1, v1, 0.f);
-    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-      float s2[2] = {0.f, 0.f};
-      kde_mfma32_sums(kq32, ch * (cb >> 1), ch * (cb >> 1) + (cb >> 1), bt0, bt1, ct0, ct1, lane, s2);
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2[0]), __float_as_uint(s2[1]), false, false);
-      const float cs = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-      L.scr[ch * WAVE + lane] = cs;
-      tot += (double)cs;
-    }
-  } else {
-    KdeOps o;
-    kde_operands(L, slots, scl, nf, o);
-    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-      float s[4] = {0.f, 0.f, 0.f, 0.f};
-      kde_sums(kq, ch * cb, ch * cb + cb, o, nf, lane, s);
-      const float cs = kde_reduce_tiles(s, lane);
-      L.scr[ch * WAVE + lane] = cs;
-      tot += (double)cs;
-    }
-  }
-  const int nfr = k32 ? -1 : nf;                      // replica form of the pass-1 elements
-  const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
-  // per-point records (4 weight-0 rows before the first point), then the reversed copy
-  const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
-  float shift = 0.f;
-  if (!(tot > 0.0)) {                                 // every weight underflowed (or NaN parent)
-    float amax = -INFINITY;
-    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nfr));
-    shift = amax;
-    tot = 0.0;
-    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-      const int j0 = min(M, ch * cb * 16), j1 = min(M, j0 + cb * 16);
-      float cs = 0.f;
-      for (int j = j0; j < j1; ++j)
-        cs += __builtin_amdgcn_exp2f(kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nfr) - shift);
-      L.scr[ch * WAVE + lane] = cs;
-      tot += (double)cs;
-    }
-  }
-  const double thr = (double)ucat * tot;
-  double cum = 0.0;
-  int ch = KDE_CHUNKS - 1;
-  for (int c2 = 0; c2 < KDE_CHUNKS; ++c2) {
-    const double nx = cum + (double)L.scr[c2 * WAVE + lane];
-    if (nx > thr) { ch = c2; break; }
-    cum = nx;
-  }
-  const int j0 = min(M, ch * cb * 16), j1 = min(M, j0 + cb * 16);
-#ifdef VBN_ABL_NOSCAN
-  wave_sync();
-  return min(j0, M - 1);
-#endif
-  const float rem = (float)(thr - cum);
-  const float csum = L.scr[ch * WAVE + lane];
-  const float4* __restrict__ rev = rec + (((M + 15) >> 4) * 16 + KDE_REC_TAIL);
-  int idx;
-  // the replica chain per feature count, compile-time (kde_arg_rec)
-  if (nfr == -1)
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
-                   [&](const float4 r) { return fmaf(r.y, -1.f, fmaf(r.x, xb0, negsq)); });
-  else if (nfr == 1)
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
-                   [&](const float4 r) { return fmaf(1.f, negsq, fmaf(r.y, -1.f, fmaf(r.x, xb0, 0.f))); });
-  else if (nfr == 2)
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift, [&](const float4 r) {
-      return fmaf(1.f, negsq, fmaf(r.z, -1.f, fmaf(r.y, xb1, fmaf(r.x, xb0, 0.f))));
-    });
-  else
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift, [&](const float4 r) {
-      return fmaf(r.w, -1.f, fmaf(r.z, xb2, fmaf(r.y, xb1, fmaf(r.x, xb0, negsq))));
-    });
-  wave_sync();
-  return idx;
-}
-
-// log p(x | parents) of a KDE node on MFMA (kde.py:114-146):
-//   root:     LSE_j log K_y - log M
-//   non-root: LSE_j (log K_p + log K_y) - LSE_j log K_p
-// pack kq (parent features) and kqy (parent ++ target features, scales c_p / c_y).  Returns
-// false (nothing added) when a sum underflows; the caller then takes the shifted VALU path.
-__device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L, bool root, float c_p,
-                                              float c_y, float cy, float log_n, float& lp) {
-  const int M = st.k, dp = st.aux0, D = st.out_dim, lane = L.lane;
-  const int nb = (((M + 15) >> 4) + 3) & ~3;
-  int slots[4] = {0, 0, 0, 0};
-  float scl[4] = {c_p, c_p, c_p, c_p};
-  for (int f = 0; f < dp; ++f) slots[f] = L.ic[st.in_off + f];
-  for (int d = 0; d < D; ++d) { slots[dp + d] = st.out_col + d; scl[dp + d] = c_y; }
-  float sy4[4] = {0.f, 0.f, 0.f, 0.f}, sp4[4] = {0.f, 0.f, 0.f, 0.f};
-  {
-    KdeOps oy;
-    kde_operands(L, slots, scl, dp + D, oy);
-    kde_sums(L.P + st.reserved[2], 0, nb, oy, dp + D, lane, sy4);
-  }
-  const float sy = kde_reduce_tiles(sy4, lane);
-  float sp = 1.f;
-  if (!root) {
-    KdeOps op;
-    kde_operands(L, slots, scl, dp, op);
-    kde_sums(L.P + st.reserved[1], 0, nb, op, dp, lane, sp4);
-    sp = kde_reduce_tiles(sp4, lane);
-  }
-  wave_sync();
-  if (!(sy > 0.f) || !(sp > 0.f)) return false;
-  lp += root ? (__logf(sy) + cy - log_n) : ((__logf(sy) - __logf(sp)) + cy);
-  return true;
-}
-
-// ---- pairwise kernel weights on VALU (alternative path, VBN_F_KDE_VALU) ---------------------
-// -|x' - y'|^2 with packed f32 VALU (v_pk_add / v_pk_mul / v_pk_fma on two points per lane),
-// points wave-uniform from scalar loads.  Measured on MI355X (cfg4, 64-node KDE, M = 10k,
-// 4096 x 1024 particles): 253 ms per walk vs 245 ms with the MFMA distance tile (and 266 ms
-// with the scalar loads software-pipelined), so the MFMA tile is the default.
-// Pack kv (plan.py _kde_pack_valu): [KDE_CHUNKS * csz / 8][NF][8] fp32, padding points
-// y' = 1e15 (weight 0).  Chunk ch = points [ch * csz, (ch + 1) * csz).
-__device__ __forceinline__ int kde_csz(int M) { return (((M + KDE_CHUNKS - 1) / KDE_CHUNKS) + 7) & ~7; }
-
-// -|x' - y'|^2 of one point record r = (y'_0, y'_1, y'_2, .); same operations, same order as
-// the packed pass (bit-identical per element)
-template <int NF>
-__device__ __forceinline__ float kde_arg_valu(const float (&xv)[4], const float4 r) {
-#pragma clang fp contract(off)
-  const float d0 = xv[0] - r.x;
-  float a = d0 * d0;
-  if (NF > 1) { const float d1 = xv[1] - r.y; a = fmaf(d1, d1, a); }
-  if (NF > 2) { const float d2 = xv[2] - r.z; a = fmaf(d2, d2, a); }
-  return -a;
-}
-
-template <int NF>
-__device__ __forceinline__ int kde_index_valu(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
-                                              float ucat, float c_p) {
-#pragma clang fp contract(off)
-  const float* __restrict__ kv = L.P + st.reserved[4];
-  const int M = st.k, lane = L.lane, csz = kde_csz(M);
-  float xv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int f = 0; f < NF; ++f) xv[f] = c_p * vread(L, L.ic[st.in_off + f]);
-  f32x2 xp[NF];
-#pragma unroll
-  for (int f = 0; f < NF; ++f) xp[f] = f32x2{xv[f], xv[f]};
-  double tot = 0.0;
-  for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-    const float* __restrict__ blk = kv + (int64_t)(ch * (csz >> 3)) * (NF * 8);
-    f32x2 acc = f32x2{0.f, 0.f};
-    for (int b = 0; b < (csz >> 3); ++b, blk += NF * 8) {
-#pragma unroll
-      for (int i = 0; i < 8; i += 2) {
-        const f32x2 d0 = xp[0] - f32x2{blk[i], blk[i + 1]};
-        f32x2 a = d0 * d0;
-        if (NF > 1) {
-          const f32x2 d1 = xp[1] - f32x2{blk[8 + i], blk[8 + i + 1]};
-          a = __builtin_elementwise_fma(d1, d1, a);
-        }
-        if (NF > 2) {
-          const f32x2 d2 = xp[2] - f32x2{blk[16 + i], blk[16 + i + 1]};
-          a = __builtin_elementwise_fma(d2, d2, a);
-        }
-        acc += f32x2{__builtin_amdgcn_exp2f(-a.x), __builtin_amdgcn_exp2f(-a.y)};
-      }
-    }
-    const float cs = acc.x + acc.y;
-    L.scr[ch * WAVE + lane] = cs;
-    tot += (double)cs;
-  }
-  // per-point records (4 weight-0 rows before the first point), then the reversed copy
-  const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
-  float shift = 0.f;
-  if (!(tot > 0.0)) {                                 // every weight underflowed (or NaN parent)
-    float amax = -INFINITY;
-    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_valu<NF>(xv, rec[j]));
-    shift = amax;
-    tot = 0.0;
-    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-      const int j0 = min(M, ch * csz), j1 = min(M, j0 + csz);
-      float cs = 0.f;
-      for (int j = j0; j < j1; ++j) cs += __builtin_amdgcn_exp2f(kde_arg_valu<NF>(xv, rec[j]) - shift);
-      L.scr[ch * WAVE + lane] = cs;
-      tot += (double)cs;
-    }
-  }
-  const double thr = (double)ucat * tot;
-  double cum = 0.0;
-  int ch = KDE_CHUNKS - 1;
-  for (int c2 = 0; c2 < KDE_CHUNKS; ++c2) {
-    const double nx = cum + (double)L.scr[c2 * WAVE + lane];
-    if (nx > thr) { ch = c2; break; }
-    cum = nx;
-  }
-  const int j0 = min(M, ch * csz), j1 = min(M, j0 + csz);
-  const float rem = (float)(thr - cum);
-  const float csum = L.scr[ch * WAVE + lane];
-  const float4* __restrict__ rev = rec + (((M + 15) >> 4) * 16 + KDE_REC_TAIL);
-  const int idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
-                           [&](const float4 r) { return kde_arg_valu<NF>(xv, r); });
-  wave_sync();
-  return idx;
-}
-
-template <int DP, int DY>
-__device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
-#pragma clang fp contract(off)
-  const float* __restrict__ P = L.P;
-  const float* __restrict__ pts = P + st.off_pts;
-  const int M = st.k, dp = DP >= 0 ? DP : st.aux0, stride = st.aux1, D = DY > 0 ? DY : st.out_dim;
-  const float* t = P + st.off_tail;
-  const float inv_sp = t[0], inv_sy = t[1], noise_scale = t[2], cy = t[3], log_n = t[4];
-  const float c_p = t[5], c_y = t[6];
-  const bool root = (st.flags & VBN_F_ROOT) != 0;
-  const int lane = L.lane;
-  float pv[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < (DP > 0 ? DP : 0); ++i) pv[i] = vread(L, L.ic[st.in_off + i]);
-
-  if (st.role == VBN_ROLE_LATENT) {
-    const float ucat = draw_uniforms(A, st, 0, L).x;
-    int idx;
-    if (root) {
-      idx = min((int)(ucat * (float)M), M - 1);             // randint(0, M)
-    } else if (st.reserved[4] >= 0 && (st.flags & VBN_F_KDE_VALU)) {
-      idx = st.aux0 == 1 ? kde_index_valu<1>(A, st, L, ucat, c_p)
-          : (st.aux0 == 2 ? kde_index_valu<2>(A, st, L, ucat, c_p) : kde_index_valu<3>(A, st, L, ucat, c_p));
-    } else if (st.reserved[1] >= 0) {
-      idx = kde_index_mfma(A, st, L, ucat, c_p);
-    } else {
-      // pass 1: per-chunk weight sums -> scr[chunk][lane]
-      const int csz = (M + KDE_CHUNKS - 1) / KDE_CHUNKS;
-      double tot = 0.0;
-      float qmin = INFINITY;
-      for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-        const int j0 = ch * csz, j1 = min(M, j0 + csz);
-        float cs = 0.f;
-        for (int j = j0; j < j1; ++j) {
-          const float q = kde_qp<DP>(pts + (int64_t)j * stride, pv, inv_sp, dp, A, st, L);
-          qmin = fminf(qmin, q);
-          cs += __expf(-0.5f * q);
-        }
-        L.scr[ch * WAVE + lane] = cs;
-        tot += (double)cs;
-      }
-      float shift = 0.f;
-      if (!(tot > 0.0)) {                                 // all weights underflowed
-        shift = qmin;
-        tot = 0.0;
-        for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-          const int j0 = ch * csz, j1 = min(M, j0 + csz);
-          float cs = 0.f;
-          for (int j = j0; j < j1; ++j)
-            cs += __expf(-0.5f * (kde_qp<DP>(pts + (int64_t)j * stride, pv, inv_sp, dp, A, st, L) - shift));
-          L.scr[ch * WAVE + lane] = cs;
-          tot += (double)cs;
-        }
-      }
-      // pass 2: locate the chunk, then scan inside it (per-lane chunk; vector loads)
-      const double thr = (double)ucat * tot;
-      double cum = 0.0;
-      int ch = KDE_CHUNKS - 1;
-      for (int c2 = 0; c2 < KDE_CHUNKS; ++c2) {
-        const double nx = cum + (double)L.scr[c2 * WAVE + lane];
-        if (nx > thr) { ch = c2; break; }
-        cum = nx;
-      }
-      const int j0 = ch * csz, j1 = min(M, j0 + csz);
-      const float rem = (float)(thr - cum);
-      float cs = 0.f;
-      idx = max(j1 - 1, 0);
-      for (int j = j0; j < j1; ++j) {
-        cs += __expf(-0.5f * (kde_qp<DP>(pts + (int64_t)j * stride, pv, inv_sp, dp, A, st, L) - shift));
-        if (cs > rem) { idx = j; break; }
-      }
-      wave_sync();
-    }
-    for (int d = 0; d < D; ++d) {
-      const float sel = pts[(int64_t)idx * stride + dp + d];
-      vwrite(L, st.out_col + d, sel + draw_normal(A, st, d, L) * noise_scale);
-    }
-  } else {
-    for (int d = 0; d < D; ++d) vwrite(L, st.out_col + d, node_fixed(A, st, d, L));
-  }
-
-  if ((st.flags & VBN_F_LOGP) && st.reserved[2] >= 0 && (root || st.reserved[1] >= 0)) {
-    wave_sync();
-    if (kde_logp_mfma(st, L, root, c_p, c_y, cy, log_n, lp)) return;
-  }
-  if (st.flags & VBN_F_LOGP) {
-    const float x0 = NODE_X(0);
-    float sy = 0.f, sp = 0.f, qymin = INFINITY, qpmin = INFINITY, qsmin = INFINITY;
-    for (int j = 0; j < M; ++j) {
-      const float* pt = pts + (int64_t)j * stride;
-      const float qy = kde_qy<DY>(pt + dp, x0, inv_sy, D, st, L);
-      if (root) {
-        sy += __expf(-0.5f * qy);
-        qymin = fminf(qymin, qy);
-      } else {
-        const float qp = kde_qp<DP>(pt, pv, inv_sp, dp, A, st, L);
-        sp += __expf(-0.5f * qp);
-        sy += __expf(-0.5f * (qp + qy));
-        qpmin = fminf(qpmin, qp);
-        qsmin = fminf(qsmin, qp + qy);
-      }
-    }
-    float sh_y = 0.f, sh_p = 0.f;
-    if (!(sy > 0.f) || (!root && !(sp > 0.f))) {   // underflow: re-sum relative to the minimum
-      sh_y = root ? qymin : qsmin;
-      sh_p = qpmin;
-      sy = 0.f;
-      sp = 0.f;
-      for (int j = 0; j < M; ++j) {
-        const float* pt = pts + (int64_t)j * stride;
-        const float qy = kde_qy<DY>(pt + dp, x0, inv_sy, D, st, L);
-        if (root) {
-          sy += __expf(-0.5f * (qy - sh_y));
-        } else {
-          const float qp = kde_qp<DP>(pt, pv, inv_sp, dp, A, st, L);
-          sp += __expf(-0.5f * (qp - sh_p));
-          sy += __expf(-0.5f * (qp + qy - sh_y));
-        }
-      }
-    }
-    const float ls_y = logf(sy) - 0.5f * sh_y;
-    if (root) {
-      lp += ls_y + cy - log_n;
-    } else {
-      const float ls_p = logf(sp) - 0.5f * sh_p;
-      lp += (ls_y - ls_p) + cy;
-    }
-  }
-}
-
-__device__ __forceinline__ void step_kde(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
-  if (st.out_dim == 1) {
-    switch (st.aux0) {
-      case 0: step_kde_t<0, 1>(A, st, L, lp); return;
-      case 1: step_kde_t<1, 1>(A, st, L, lp); return;
-      case 2: step_kde_t<2, 1>(A, st, L, lp); return;
-      case 3: step_kde_t<3, 1>(A, st, L, lp); return;
-      default: break;
-    }
-  }
-  step_kde_t<-1, -1>(A, st, L, lp);
-}
-
-// ------------------------------------------------------------------------------------------
-// Gibbs sweep steps (gibbs.py:40-87): lanes 8c .. 8c+7 hold chain c's 8 candidates
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void gibbs_select(const vbn_walk_args& A, const vbn_step& st, Lane& L, float lp) {
-  const int lane = L.lane, g0 = lane & ~7;
-  float m = fmaxf(lp, __shfl_xor(lp, 1));
-  m = fmaxf(m, __shfl_xor(m, 2));
-  m = fmaxf(m, __shfl_xor(m, 4));
-  const float e = __expf(lp - m);                       // softmax(log_score, 1) (79)
-  float se = e + __shfl_xor(e, 1);
-  se += __shfl_xor(se, 2);
-  se += __shfl_xor(se, 4);
-  float pk[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) pk[k] = __shfl(e, g0 + k) / se;
-  // one uniform per chain (candidate lane 0's draw), multinomial(weights, 1) (80); without
-  // injected noise it comes from the node's own SELECT stream, which no candidate draw uses
-  const int s_keep = L.s;
-  L.s = 0;
-  const float u = A.noise ? draw_uniforms(A, st, 0, L).x : u01(rng_words(A, st, 0, RNG_SELECT, L).x);
-  L.s = s_keep;
-  const int idx = inv_cdf(8, u, [&](int k) { return pk[k]; });
-  for (int d = 0; d < st.out_dim; ++d) {
-    const float v = __shfl(vread(L, st.out_col + d), g0 + idx);
-    wave_sync();
-    vwrite(L, st.out_col + d, v);                        // chosen candidate (81-82)
-  }
-}
-
-__device__ __forceinline__ void gibbs_collect(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
-  const int it = L.iter, burn = A.gibbs_burn_in, thin = max(A.gibbs_thin, 1);
-  if (it < burn || (it - burn) % thin != 0 || L.s != 0 || !L.valid || (L.mirror && L.lane >= 32)) return;  // 83-87
-  const int n_collect = (A.gibbs_iters - burn + thin - 1) / thin;
-  const int k = (it - burn) / thin;
-  for (int d = 0; d < st.out_dim; ++d)
-    A.out_x[(L.b * n_collect + k) * A.n_out_cols + d] = vread(L, st.out_col + d);
-}
-
-// ------------------------------------------------------------------------------------------
-// the walk
-// ------------------------------------------------------------------------------------------
-// One step of the walk for the wave's 64 particles.
-// KM: bit0 gaussian_nn, bit1 linear_gaussian, bit2 mdn, bit3 kde, bit4 softmax_nn,
-// bit5 non-relu activations.  Each instantiation only carries the code (and registers) of
-// the CPD kinds a plan uses.
-template <unsigned KM>
-__device__ __forceinline__ void walk_step(const vbn_walk_args& A, const vbn_step& st, Lane& L, float& lp) {
-  if (st.role == VBN_ROLE_SKIP) return;
-  if (st.flags & VBN_F_LPRESET) lp = 0.f;
-  if (st.role == VBN_ROLE_SELECT) {
-    gibbs_select(A, st, L, lp);
-    wave_sync();
-    return;
-  }
-  if (st.role == VBN_ROLE_COLLECT) {
-    gibbs_collect(A, st, L);
-    return;
-  }
-  if (st.role == VBN_ROLE_FIXED && !(st.flags & VBN_F_LOGP)) {   // evidence / do: value only
-    for (int d = 0; d < st.out_dim; ++d) vwrite(L, st.out_col + d, node_fixed(A, st, d, L));
-    wave_sync();
-    return;
-  }
-  switch (st.kind) {
-    case VBN_KIND_GAUSSIAN_NN: if constexpr ((KM & 1) != 0) step_gaussian_nn<KM>(A, st, L, lp); break;
-    case VBN_KIND_LINEAR_GAUSSIAN: if constexpr ((KM & 2) != 0) step_linear_gaussian(A, st, L, lp); break;
-    case VBN_KIND_MDN: if constexpr ((KM & 4) != 0) step_mdn<KM>(A, st, L, lp); break;
-    case VBN_KIND_KDE: if constexpr ((KM & 8) != 0) step_kde(A, st, L, lp); break;
-    default: if constexpr ((KM & 16) != 0) step_softmax_nn<KM>(A, st, L, lp); break;
-  }
-  wave_sync();
-}
-
-typedef __attribute__((address_space(3))) void lds_void;
-// Staged walks (kind sets of gaussian_nn / linear_gaussian only): NN weight blocks are DMA'd
-// into LDS one step ahead and shared by the 4 waves of a workgroup, one barrier per step.
-// Measured on MI355X (walk ms, staged vs direct): cfg2 1.22 vs 1.35; with mdn/softmax_nn heads
-// (cfg3) 4.43 vs 4.26 and with KDE nodes (cfg5) 186 vs 166 (per-wave work varies by node, the
-// barrier waits for the slowest wave) -- those kind sets read the blob straight (L1/L2).
-#ifndef VBN_STAGE
-#define VBN_STAGE 1
-#endif
-__host__ __device__ constexpr bool staged_kinds(unsigned km) { return VBN_STAGE && (km & 28u) == 0; }
-#define WG_MAX_WAVES 4
-#define WBLK_CHUNK 256   // floats per global_load_lds_dwordx4 wave instruction (64 lanes x 16 B)
-
-// Stage step j's NN weight block into LDS weight buffer ``buf``: the workgroup's waves split
-// its 1-KiB chunks, one global_load_lds_dwordx4 each (no VGPRs; completion is waited for by
-// step_barrier before the step that reads it).
-__device__ __forceinline__ void stage_block(const vbn_walk_args& A, const vbn_step* __restrict__ steps,
-                                            const float* __restrict__ params, float* wbuf, int j, int buf,
-                                            int wave, int nw, int lane) {
-  const int off = steps[j].reserved[5], len = steps[j].reserved[6];
-  if (len <= 0) return;
-  float* dst = wbuf + buf * A.wbuf_floats;
-  for (int c = wave; c * WBLK_CHUNK < len; c += nw)
-    __builtin_amdgcn_global_load_lds((const void*)(params + off + c * WBLK_CHUNK + lane * 4),
-                                     (lds_void*)(dst + c * WBLK_CHUNK), 16, 0, 0);
-}
-
-// end of a step: this wave's LDS-DMA has landed, every wave of the workgroup is done with the
-// buffer the next step's prefetch overwrites
-__device__ __forceinline__ void step_barrier() {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef VBN_ABL_NOBAR
-  return;
-#endif
-  __syncthreads();
-}
-
-// The walk.  A workgroup = nw (1, 2 or 4; blockDim.x / 64) waves, each owning 64 consecutive
-// particles with its own LDS value slots; the waves walk the same step table in lockstep (one
-// barrier per step) and share two LDS weight buffers: while step i runs on buffer i & 1, step
-// i + 1's MLP weights are DMA'd into the other one (one memory latency per step, hidden
-// behind the step's compute, and one copy per workgroup instead of per wave).
-#ifndef VBN_WPE
-#define VBN_WPE 4
-#endif
-template <unsigned KM>
-__global__ void __launch_bounds__(WG_MAX_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(VBN_WPE)))
-vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const vbn_step* __restrict__ steps,
-                const int32_t* __restrict__ in_cols) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6;
-  const int per_wave = (A.n_slots + (A.max_out > 0 ? A.max_out : 1)) * WAVE;
-  float* wbuf = smem + nw * per_wave;
-  Lane L;
-  L.P = params;
-  L.ic = in_cols;
-  L.lane = threadIdx.x & (WAVE - 1);
-  L.vals = smem + wave * per_wave;
-  L.scr = L.vals + A.n_slots * WAVE;
-  L.wb = wbuf;
-  const int64_t total = A.n_queries * (int64_t)A.n_samples;
-  // half-wave launches (wave_particles 32): lane l and l + 32 carry the same particle, so
-  // every draw and value agrees; only the lower half writes, the MLPs run group 0 only
-  L.mirror = A.wave_particles == 32;
-  const int wp = L.mirror ? 32 : WAVE;
-  const int64_t p_raw = ((int64_t)blockIdx.x * nw + wave) * wp + (L.lane & (wp - 1));
-  const bool valid = p_raw < total;
-  L.p = valid ? p_raw : total - 1;
-  L.b = L.p / A.n_samples;
-  L.s = (int)(L.p - L.b * A.n_samples);
-  L.iter = 0;
-  L.valid = valid;
-
-  float lp = 0.f;
-  if (A.state && (A.state_flags & 1)) {             // resume a segmented walk
-    for (int c = 0; c < A.n_slots; ++c) vwrite(L, c, A.state[(int64_t)c * total + L.p]);
-    lp = A.state[(int64_t)A.n_slots * total + L.p];
-    wave_sync();
-  }
-  const int iters = A.mode == VBN_MODE_GIBBS ? A.gibbs_iters : 1;
-  if constexpr (staged_kinds(KM)) {
-  int par = 0;
-  if (A.n_steps > 0) stage_block(A, steps, params, wbuf, 0, 0, wave, nw, L.lane);
-  step_barrier();
-  for (int it = 0; it < iters; ++it) {
-    L.iter = it;
-    for (int i = 0; i < A.n_steps; ++i) {
-      const bool last = i + 1 == A.n_steps;
-      if (!last || it + 1 < iters) stage_block(A, steps, params, wbuf, last ? 0 : i + 1, par ^ 1, wave, nw, L.lane);
-      L.wb = wbuf + par * A.wbuf_floats;
-      walk_step<KM>(A, steps[i], L, lp);
-      step_barrier();
-      par ^= 1;
-    }
-  }
-  } else {
-  (void)wbuf;
-  for (int it = 0; it < iters; ++it) {
-    L.iter = it;
-    for (int i = 0; i < A.n_steps; ++i) {
-      const vbn_step st = steps[i];
-      L.wb = params + st.reserved[5];
-      walk_step<KM>(A, st, L, lp);
-    }
-  }
-  }
-  if (!valid || (L.mirror && L.lane >= 32)) return;
-  if (A.mode == VBN_MODE_GIBBS) return;                  // outputs written by COLLECT steps
-  if (A.state && (A.state_flags & 2)) {
-    for (int c = 0; c < A.n_slots; ++c) A.state[(int64_t)c * total + L.p] = vread(L, c);
-    A.state[(int64_t)A.n_slots * total + L.p] = lp;
-  }
-  if (A.out_lp && A.mode != VBN_MODE_SAMPLE) A.out_lp[L.p] = (A.mode == VBN_MODE_MCM) ? __expf(lp) : lp;
-  if (A.out_x) {
-    for (int k = 0; k < A.n_out_cols; ++k)
-      A.out_x[L.p * A.n_out_cols + k] = vread(L, A.out_cols[k]);
-  }
-}
-
+// vbn_walk.hip — host entry points of the C-ABI (include/vbn_hip.h) and the small kernels
+// (weight normalisation, RB epilogue, resampling, posterior statistics).  The walk kernel
+// lives in vbn_walk_impl.h; its kind-set instantiations are compiled one per object from
+// walk_inst.hip and launched through vbn_launch_walk_km<KM>.
+#include "vbn_walk_impl.h"
+
+// the walk launchers, one per object compiled from walk_inst.hip
+#define VBN_DECL(K) extern "C" hipError_t vbn_launch_walk_km##K(const vbn_walk_args*, dim3, dim3, size_t, hipStream_t);
+VBN_WALK_KIND_SETS(VBN_DECL)
+#undef VBN_DECL
 // ------------------------------------------------------------------------------------------
 // per-query weight normalisation (softmax over S + ESS, or max-shifted exp)
 // ------------------------------------------------------------------------------------------
@@ -1957,7 +315,7 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   if (a->wave_particles != 0 && a->wave_particles != 32 && a->wave_particles != WAVE)
     return fail(VBN_E_ARGS, "vbn_hip_walk: wave_particles must be 0, 32 or 64");
   const int64_t wp = a->wave_particles == 32 ? 32 : WAVE;   // particles per wave
-  // smallest instantiated kind set covering the plan
+  // smallest instantiated kind set covering the plan (VBN_WALK_KIND_SETS)
   static const unsigned masks[] = {1u, 2u, 3u, 4u, 8u, 16u, 20u, 23u, 31u, 63u};
   const unsigned want = (unsigned)a->kind_mask & 63u;
   unsigned km = 63u;
@@ -1994,26 +352,22 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
   const dim3 grid((unsigned)blocks), block(WAVE * nw);
   hipStream_t st = (hipStream_t)stream;
+  // kind set | 64: the half-wave (mirror) instantiation
+  const unsigned kmi = km | (wp == 32 ? 64u : 0u);
+  hipError_t e = hipErrorInvalidDeviceFunction;
 #ifdef VBN_KM_ONLY
   // experiment builds (make exp KM=...): one instantiation only
-  if ((VBN_KM_ONLY & want) != want) return fail(VBN_E_ARGS, "vbn_hip_walk: kind set not built in this experiment library");
-  hipLaunchKernelGGL(vbn_walk_kernel<(unsigned)VBN_KM_ONLY>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols);
-  (void)km;
+  if ((VBN_KM_ONLY & want) != want || kmi != (unsigned)VBN_KM_ONLY)
+    return fail(VBN_E_ARGS, "vbn_hip_walk: kind set not built in this experiment library");
+  e = VBN_LAUNCHER(VBN_KM_ONLY)(a, grid, block, (size_t)lds, st);
 #else
-  switch (km) {
-    case 1u: hipLaunchKernelGGL(vbn_walk_kernel<1u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
-    case 2u: hipLaunchKernelGGL(vbn_walk_kernel<2u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
-    case 3u: hipLaunchKernelGGL(vbn_walk_kernel<3u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
-    case 4u: hipLaunchKernelGGL(vbn_walk_kernel<4u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
-    case 8u: hipLaunchKernelGGL(vbn_walk_kernel<8u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
-    case 16u: hipLaunchKernelGGL(vbn_walk_kernel<16u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
-    case 20u: hipLaunchKernelGGL(vbn_walk_kernel<20u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
-    case 23u: hipLaunchKernelGGL(vbn_walk_kernel<23u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
-    case 31u: hipLaunchKernelGGL(vbn_walk_kernel<31u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
-    default: hipLaunchKernelGGL(vbn_walk_kernel<63u>, grid, block, (size_t)lds, st, *a, a->params, a->steps, a->in_cols); break;
+  switch (kmi) {
+#define VBN_CASE(K) case K##u: e = vbn_launch_walk_km##K(a, grid, block, (size_t)lds, st); break;
+    VBN_WALK_KIND_SETS(VBN_CASE)
+#undef VBN_CASE
+    default: break;
   }
 #endif
-  const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;
 }
