@@ -1,6 +1,6 @@
 """Host-side plan logic: liveness slot allocation and MFMA fragment packing.
 
-``emulate_mlp`` replays csrc/vbn_walk.hip's mlp_forward data flow in numpy with the
+``emulate_mlp`` replays csrc/vbn_walk_impl.h's mlp_forward data flow in numpy with the
 documented gfx950 lane layouts of v_mfma_f32_32x32x2_f32 (A[i=l&31][k=l>>5],
 B[k=l>>5][j=l&31], D row (r&3)+8(r>>2)+4(l>>5), col l&31) and v_permlane32_swap, so the
 packed parameter blocks are checked against torch's MLP without a GPU.

@@ -6,7 +6,7 @@ slices, evidence/do masks) and re-reads CPD parameters inside every ATen call.  
 work is split in two device-resident objects:
 
 * :class:`PackedModel` — once per model and device: every CPD's parameters packed into one
-  fp32 blob in the fragment layouts the kernel reads (see ``csrc/vbn_walk.hip``), plus the
+  fp32 blob in the fragment layouts the kernel reads (see ``csrc/vbn_walk_impl.h``), plus the
   host-side constants the reference recomputes per call (root loc/scale, mixture weights,
   KDE kernel scales), computed with the same torch fp32 ops so they are bit-identical.
 * :class:`QueryPlan` — once per (query signature, engine mode): the ``vbn_step`` table
@@ -86,7 +86,7 @@ def _kde_cb(m: int) -> int:
 
 
 def _kde_pack(feats: List[np.ndarray], records: bool = False) -> np.ndarray:
-    """KDE point features y' (scaled) for the kernel (csrc/vbn_walk.hip, kde_mfma_sums).
+    """KDE point features y' (scaled) for the kernel (csrc/vbn_walk_impl.h, kde_mfma_sums).
 
     MFMA A-operand image: [KDE_CHUNKS * cb][4][16] fp32 (cb = _kde_cb(M) blocks per chunk),
     columns (y'_0 .. y'_{nf-1}, |y'|^2, 1) for nf <= 2 and (y'_0, y'_1, y'_2, |y'|^2) for
@@ -148,7 +148,7 @@ def _np(t: torch.Tensor) -> np.ndarray:
 
 
 def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
-    """MFMA fragment layouts of csrc/vbn_walk.hip mlp_forward (biases as accumulator init)."""
+    """MFMA fragment layouts of csrc/vbn_walk_impl.h mlp_forward (biases as accumulator init)."""
     layers = rec.mlp_layers()
     hidden = tuple(int(w.shape[0]) for w, _ in layers[:-1])
     if hidden != MLP_HIDDEN:
@@ -282,7 +282,7 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
         c_y = np.float32(_KDE_C / s_y)
         offs["tail"] = blob.add(np.array([1.0 / np.float32(s_p), 1.0 / np.float32(s_y),
                                           noise_scale, cy, math.log(float(m)), c_p, c_y, 0], np.float32))
-        # MFMA packs (csrc/vbn_walk.hip, kde_mfma_sums): [block][k][16] point features
+        # MFMA packs (csrc/vbn_walk_impl.h, kde_mfma_sums): [block][k][16] point features
         if 1 <= dp <= 3:
             offs["kq"] = blob.add(_kde_pack([_np(pts_p) * c_p]))
             offs["kr"] = blob.add(_kde_pack([_np(pts_p) * c_p], records=True))
