@@ -352,13 +352,16 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
   const dim3 grid((unsigned)blocks), block(WAVE * nw);
   hipStream_t st = (hipStream_t)stream;
-  // kind set | 64: the half-wave (mirror) instantiation
-  const unsigned kmi = km | (wp == 32 ? 64u : 0u);
+  // kind set | 64: the half-wave (mirror) instantiation; | 128: the lean one
+  const bool lean = !a->noise && !a->state && a->mode != VBN_MODE_GIBBS;
+  const unsigned kmi = km | (wp == 32 ? 64u : 0u) | (lean && wp != 32 ? 128u : 0u);
   hipError_t e = hipErrorInvalidDeviceFunction;
 #ifdef VBN_KM_ONLY
   // experiment builds (make exp KM=...): one instantiation only
-  if ((VBN_KM_ONLY & want) != want || kmi != (unsigned)VBN_KM_ONLY)
+  // (a lean-less set may serve a lean launch; never the reverse)
+  if ((VBN_KM_ONLY & want) != want || ((VBN_KM_ONLY & 64) != 0) != (wp == 32) || ((VBN_KM_ONLY & 128) && !lean))
     return fail(VBN_E_ARGS, "vbn_hip_walk: kind set not built in this experiment library");
+  (void)kmi;
   e = VBN_LAUNCHER(VBN_KM_ONLY)(a, grid, block, (size_t)lds, st);
 #else
   switch (kmi) {

@@ -120,7 +120,9 @@ struct Lane {
   int s;         // sample (Gibbs: candidate)
   int iter;      // Gibbs sweep (0 for every other walk)
   bool valid;    // particle index inside the batch
-  bool mirror;   // half-wave launch: lanes 32-63 mirror lanes 0-31 (wave-uniform)
+  bool mirror;   // half-wave launch: lanes 32-63 mirror lanes 0-31 (kind-set bit 6)
+  bool lean;     // no injected draws, no segment state, not Gibbs (kind-set bit 7): the
+                 // kernel sets both from KM, so every inlined check on them folds away
 };
 
 // Draws of node ``st``, dimension d, for this particle.  Stream 0 gives a standard normal
@@ -153,7 +155,7 @@ __device__ __forceinline__ int64_t noise_index(const vbn_walk_args& A, const vbn
 }
 
 __device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
-  if (A.noise) return A.noise[noise_index(A, st, d, 1, L)];
+  if (!L.lean && A.noise) return A.noise[noise_index(A, st, d, 1, L)];
 #ifdef VBN_ABL_NORNG
   return 0.5f;
 #endif
@@ -163,7 +165,8 @@ __device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_s
 
 // (categorical uniform, within-bin uniform)
 __device__ __forceinline__ float2 draw_uniforms(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
-  if (A.noise) return make_float2(A.noise[noise_index(A, st, d, 0, L)], A.noise[noise_index(A, st, d, 1, L)]);
+  if (!L.lean && A.noise)
+    return make_float2(A.noise[noise_index(A, st, d, 0, L)], A.noise[noise_index(A, st, d, 1, L)]);
   const uint2 w = rng_words(A, st, d, RNG_UNIFORM, L);
   return make_float2(u01(w.x), u01(w.y));
 }
@@ -1599,6 +1602,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
   // half-wave launches (wave_particles 32): lane l and l + 32 carry the same particle, so
   // every draw and value agrees; only the lower half writes, the MLPs run group 0 only
   L.mirror = (KM & 64) != 0;                         // host: wave_particles == 32
+  L.lean = (KM & 128) != 0;                          // host: no noise, no state, not Gibbs
   const int wp = L.mirror ? 32 : WAVE;
   const int64_t p_raw = ((int64_t)blockIdx.x * nw + wave) * wp + (L.lane & (wp - 1));
   const bool valid = p_raw < total;
@@ -1609,12 +1613,12 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
   L.valid = valid;
 
   float lp = 0.f;
-  if (A.state && (A.state_flags & 1)) {             // resume a segmented walk
+  if (!L.lean && A.state && (A.state_flags & 1)) {  // resume a segmented walk
     for (int c = 0; c < A.n_slots; ++c) vwrite(L, c, A.state[(int64_t)c * total + L.p]);
     lp = A.state[(int64_t)A.n_slots * total + L.p];
     wave_sync();
   }
-  const int iters = A.mode == VBN_MODE_GIBBS ? A.gibbs_iters : 1;
+  const int iters = (!L.lean && A.mode == VBN_MODE_GIBBS) ? A.gibbs_iters : 1;
   if constexpr (staged_kinds(KM)) {
   int par = 0;
   if (A.n_steps > 0) stage_block(A, steps, params, wbuf, 0, 0, wave, nw, L.lane);
@@ -1643,7 +1647,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
   }
   if (!valid || (L.mirror && L.lane >= 32)) return;
   if (A.mode == VBN_MODE_GIBBS) return;                  // outputs written by COLLECT steps
-  if (A.state && (A.state_flags & 2)) {
+  if (!L.lean && A.state && (A.state_flags & 2)) {
     for (int c = 0; c < A.n_slots; ++c) A.state[(int64_t)c * total + L.p] = vread(L, c);
     A.state[(int64_t)A.n_slots * total + L.p] = lp;
   }
@@ -1655,10 +1659,13 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
 }
 
 // Instantiated kind sets: bits 0-4 the CPD kinds walked, bit 5 non-relu activations, bit 6 the
-// half-wave (mirror) launch (include/vbn_hip.h wave_particles = 32).  Each is compiled in its
+// half-wave (mirror) launch (include/vbn_hip.h wave_particles = 32), bit 7 the lean walk (no
+// injected draws, no segment state, not Gibbs: the production MCM / IS / LW / ancestral path;
+// measured cfg2 1.215 -> 1.19 ms, SGPR spills 35 -> 0).  Each is compiled in its
 // own object from walk_inst.hip (Makefile KIND_SETS must list the same values).
 #define VBN_WALK_KIND_SETS(X) \
   X(1) X(2) X(3) X(4) X(8) X(16) X(20) X(23) X(31) X(63) \
-  X(65) X(66) X(67) X(68) X(72) X(80) X(84) X(87) X(95) X(127)
+  X(65) X(66) X(67) X(68) X(72) X(80) X(84) X(87) X(95) X(127) \
+  X(129) X(130) X(131) X(132) X(136) X(144) X(148) X(151) X(159) X(191)
 #define VBN_LAUNCHER_(K) vbn_launch_walk_km##K
 #define VBN_LAUNCHER(K) VBN_LAUNCHER_(K)
