@@ -5,7 +5,7 @@ The local engine is a deterministic CPU stand-in with the accelerated engines' i
 seed broadcast, batch-global fallback decision and the gather exactly.
 """
 import os
-import socket
+import tempfile
 
 import pytest
 import torch
@@ -41,16 +41,13 @@ class StubEngine:
         return pdf, (pdf.unsqueeze(-1) + ev.unsqueeze(1))
 
 
-def _free_port():
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        return sk.getsockname()[1]
+def _rendezvous():
+    """A fresh file:// rendezvous for one world (no TCP port to race for between tests)."""
+    return "file://" + os.path.join(tempfile.mkdtemp(prefix="vbn_gloo_"), "store")
 
 
-def _worker(rank, world, port, ev, out_q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init, ev, out_q):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         torch.manual_seed(123 + rank)                 # ranks disagree; the seed is broadcast
         eng = ShardedEngine(StubEngine(), gather=True)
@@ -64,8 +61,8 @@ def _worker(rank, world, port, ev, out_q):
 def _run(ev, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, ev, q)) for r in range(world)]
+    init = _rendezvous()
+    procs = [ctx.Process(target=_worker, args=(r, world, init, ev, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
@@ -119,10 +116,8 @@ class StubChainSampler:
         return (torch.cos(q * 0.9 + t * 0.2 + (seed % 1000) * 1e-3) + ev.view(b, 1, 1)).float()
 
 
-def _chain_worker(rank, world, port, ev, out_q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _chain_worker(rank, world, init, ev, out_q):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         torch.manual_seed(123 + rank)
         eng = ShardedEngine(StubChainSampler(), gather=True)
@@ -137,8 +132,8 @@ def test_gloo_world2_sharded_chains_match_single_process():
     ev = torch.linspace(-1, 1, 5).unsqueeze(1)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_chain_worker, args=(r, 2, port, ev, q)) for r in range(2)]
+    init = _rendezvous()
+    procs = [ctx.Process(target=_chain_worker, args=(r, 2, init, ev, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])

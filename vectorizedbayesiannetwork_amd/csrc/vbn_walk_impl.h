@@ -183,7 +183,7 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
 // value of a fixed node: from the fixed buffer, or (VBN_F_KEEP, Gibbs) the slot's current value
 __device__ __forceinline__ float node_fixed(const vbn_walk_args& A, const vbn_step& st, int d,
                                             const Lane& L) {
-  return (st.flags & VBN_F_KEEP) ? vread(L, st.out_col + d) : fixed_value(A, st, d, L);
+  return (!L.lean && (st.flags & VBN_F_KEEP)) ? vread(L, st.out_col + d) : fixed_value(A, st, d, L);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1513,13 +1513,13 @@ __device__ __forceinline__ void gibbs_collect(const vbn_walk_args& A, const vbn_
 template <unsigned KM>
 __device__ __forceinline__ void walk_step(const vbn_walk_args& A, const vbn_step& st, Lane& L, float& lp) {
   if (st.role == VBN_ROLE_SKIP) return;
-  if (st.flags & VBN_F_LPRESET) lp = 0.f;
-  if (st.role == VBN_ROLE_SELECT) {
+  if (!L.lean && (st.flags & VBN_F_LPRESET)) lp = 0.f;
+  if (!L.lean && st.role == VBN_ROLE_SELECT) {        // Gibbs roles: not in lean walks
     gibbs_select(A, st, L, lp);
     wave_sync();
     return;
   }
-  if (st.role == VBN_ROLE_COLLECT) {
+  if (!L.lean && st.role == VBN_ROLE_COLLECT) {
     gibbs_collect(A, st, L);
     return;
   }
