@@ -354,12 +354,14 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   // kind set | 64: the half-wave (mirror) instantiation; | 128: the lean one
   const bool lean = !a->noise && !a->state && a->mode != VBN_MODE_GIBBS;
-  const unsigned kmi = km | (wp == 32 ? 64u : 0u) | (lean && wp != 32 ? 128u : 0u);
+  const unsigned kmi = km | (wp == 32 ? 64u : 0u) | (lean && wp != 32 ? 128u : 0u) |
+                       (wp == 32 && !a->noise ? 256u : 0u);   // | 256: half-wave without injected draws
   hipError_t e = hipErrorInvalidDeviceFunction;
 #ifdef VBN_KM_ONLY
   // experiment builds (make exp KM=...): one instantiation only
   // (a lean-less set may serve a lean launch; never the reverse)
-  if ((VBN_KM_ONLY & want) != want || ((VBN_KM_ONLY & 64) != 0) != (wp == 32) || ((VBN_KM_ONLY & 128) && !lean))
+  if ((VBN_KM_ONLY & want) != want || ((VBN_KM_ONLY & 64) != 0) != (wp == 32) || ((VBN_KM_ONLY & 128) && !lean) ||
+      ((VBN_KM_ONLY & 256) && a->noise))
     return fail(VBN_E_ARGS, "vbn_hip_walk: kind set not built in this experiment library");
   (void)kmi;
   e = VBN_LAUNCHER(VBN_KM_ONLY)(a, grid, block, (size_t)lds, st);

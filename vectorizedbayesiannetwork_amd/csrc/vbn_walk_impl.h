@@ -122,7 +122,8 @@ struct Lane {
   bool valid;    // particle index inside the batch
   bool mirror;   // half-wave launch: lanes 32-63 mirror lanes 0-31 (kind-set bit 6)
   bool lean;     // no injected draws, no segment state, not Gibbs (kind-set bit 7): the
-                 // kernel sets both from KM, so every inlined check on them folds away
+                 // kernel sets these from KM, so every inlined check on them folds away
+  bool noiseless;  // no injected draws (lean, or kind-set bit 8: production Gibbs)
 };
 
 // Draws of node ``st``, dimension d, for this particle.  Stream 0 gives a standard normal
@@ -155,7 +156,7 @@ __device__ __forceinline__ int64_t noise_index(const vbn_walk_args& A, const vbn
 }
 
 __device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
-  if (!L.lean && A.noise) return A.noise[noise_index(A, st, d, 1, L)];
+  if (!L.noiseless && A.noise) return A.noise[noise_index(A, st, d, 1, L)];
 #ifdef VBN_ABL_NORNG
   return 0.5f;
 #endif
@@ -165,7 +166,7 @@ __device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_s
 
 // (categorical uniform, within-bin uniform)
 __device__ __forceinline__ float2 draw_uniforms(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
-  if (!L.lean && A.noise)
+  if (!L.noiseless && A.noise)
     return make_float2(A.noise[noise_index(A, st, d, 0, L)], A.noise[noise_index(A, st, d, 1, L)]);
   const uint2 w = rng_words(A, st, d, RNG_UNIFORM, L);
   return make_float2(u01(w.x), u01(w.y));
@@ -1484,7 +1485,7 @@ __device__ __forceinline__ void gibbs_select(const vbn_walk_args& A, const vbn_s
   // injected noise it comes from the node's own SELECT stream, which no candidate draw uses
   const int s_keep = L.s;
   L.s = 0;
-  const float u = A.noise ? draw_uniforms(A, st, 0, L).x : u01(rng_words(A, st, 0, RNG_SELECT, L).x);
+  const float u = (!L.noiseless && A.noise) ? draw_uniforms(A, st, 0, L).x : u01(rng_words(A, st, 0, RNG_SELECT, L).x);
   L.s = s_keep;
   const int idx = inv_cdf(8, u, [&](int k) { return pk[k]; });
   for (int d = 0; d < st.out_dim; ++d) {
@@ -1603,6 +1604,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
   // every draw and value agrees; only the lower half writes, the MLPs run group 0 only
   L.mirror = (KM & 64) != 0;                         // host: wave_particles == 32
   L.lean = (KM & 128) != 0;                          // host: no noise, no state, not Gibbs
+  L.noiseless = (KM & (128 | 256)) != 0;             // host: no injected draws
   const int wp = L.mirror ? 32 : WAVE;
   const int64_t p_raw = ((int64_t)blockIdx.x * nw + wave) * wp + (L.lane & (wp - 1));
   const bool valid = p_raw < total;
@@ -1661,11 +1663,13 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
 // Instantiated kind sets: bits 0-4 the CPD kinds walked, bit 5 non-relu activations, bit 6 the
 // half-wave (mirror) launch (include/vbn_hip.h wave_particles = 32), bit 7 the lean walk (no
 // injected draws, no segment state, not Gibbs: the production MCM / IS / LW / ancestral path;
-// measured cfg2 1.215 -> 1.19 ms, SGPR spills 35 -> 0).  Each is compiled in its
+// measured cfg2 1.215 -> 1.19 ms, SGPR spills 35 -> 0), bit 8 no injected draws (with bit 6: the
+// production half-wave Gibbs sweeps; SGPR spills 34 -> 9).  Each is compiled in its
 // own object from walk_inst.hip (Makefile KIND_SETS must list the same values).
 #define VBN_WALK_KIND_SETS(X) \
   X(1) X(2) X(3) X(4) X(8) X(16) X(20) X(23) X(31) X(63) \
   X(65) X(66) X(67) X(68) X(72) X(80) X(84) X(87) X(95) X(127) \
-  X(129) X(130) X(131) X(132) X(136) X(144) X(148) X(151) X(159) X(191)
+  X(129) X(130) X(131) X(132) X(136) X(144) X(148) X(151) X(159) X(191) \
+  X(321) X(322) X(323) X(324) X(328) X(336) X(340) X(343) X(351) X(383)
 #define VBN_LAUNCHER_(K) vbn_launch_walk_km##K
 #define VBN_LAUNCHER(K) VBN_LAUNCHER_(K)
