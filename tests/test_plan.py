@@ -368,3 +368,39 @@ def test_kde_records_carry_a_reversed_copy():
         pad[4:4 + m] = False
         pad[4 + nb16 + KDE_REC_TAIL:4 + nb16 + KDE_REC_TAIL + m] = False
         assert (r[pad, nf] == np.float32(1e30)).all()
+
+
+def test_normal_pairs_are_consecutive_and_class_pure():
+    """plan._pair_normals: every VBN_F_BM_FIRST step is followed (not necessarily adjacently) by
+    its VBN_F_BM_SECOND step before any other FIRST, both are one-dimensional gaussian LATENT
+    steps of the same F_SHARED class, and FIXED / other-kind steps are never flagged."""
+    import networkx as nx
+    from vectorizedbayesiannetwork_amd import synthetic
+    from vectorizedbayesiannetwork_amd.model import random_init_model
+    from vectorizedbayesiannetwork_amd.plan import (F_BM_FIRST, F_BM_SECOND, F_SHARED, KIND_ID, MODE_MCM,
+                                                    ROLE_LATENT, S_FLAGS, S_KIND, S_OUTDIM, S_ROLE,
+                                                    PackedModel, build_plan)
+    g = synthetic.random_dag(20, seed=0)
+    data = synthetic.sem_data(g, 512, seed=0)
+    kinds = synthetic.round_robin_kinds(g, ["gaussian_nn", "linear_gaussian", "mdn"])
+    pk = PackedModel(random_init_model(g, kinds, data, seed=0), "cpu")
+    topo = pk.model.topo
+    ev = set(topo[3::5])
+    plan = build_plan(pk, latent=[n for n in topo if n not in ev], fixed=list(ev), logp=[topo[-1]],
+                      out_nodes=[topo[-1]], shared_roots=True, mode=MODE_MCM)
+    rows = plan.steps.cpu().numpy()
+    open_first = None
+    n_pairs = 0
+    for r in rows:
+        f = int(r[S_FLAGS])
+        if f & (F_BM_FIRST | F_BM_SECOND):
+            assert r[S_ROLE] == ROLE_LATENT and r[S_OUTDIM] == 1
+            assert r[S_KIND] in (KIND_ID["gaussian_nn"], KIND_ID["linear_gaussian"])
+        if f & F_BM_FIRST:
+            assert open_first is None
+            open_first = f & F_SHARED
+        if f & F_BM_SECOND:
+            assert open_first is not None and open_first == (f & F_SHARED)
+            open_first = None
+            n_pairs += 1
+    assert open_first is None and n_pairs >= 3

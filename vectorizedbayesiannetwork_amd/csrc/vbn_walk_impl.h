@@ -124,6 +124,7 @@ struct Lane {
   bool lean;     // no injected draws, no segment state, not Gibbs (kind-set bit 7): the
                  // kernel sets these from KM, so every inlined check on them folds away
   bool noiseless;  // no injected draws (lean, or kind-set bit 8: production Gibbs)
+  mutable float bm_spare;  // lean walks: the r sin half of a VBN_F_BM_FIRST step's Box-Muller pair
 };
 
 // Draws of node ``st``, dimension d, for this particle.  Stream 0 gives a standard normal
@@ -160,7 +161,18 @@ __device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_s
 #ifdef VBN_ABL_NORNG
   return 0.5f;
 #endif
+  // lean walks pair the dim-0 normals of consecutive one-dimensional gaussian steps (host flags,
+  // plan.py _pair_normals): the first step's Philox pair gives r cos(2 pi u2) to itself and
+  // r sin(2 pi u2) -- an independent N(0, 1) -- to the second, halving Philox + log + sqrt
+  if (L.lean && d == 0 && (st.flags & VBN_F_BM_SECOND)) return L.bm_spare;
   const uint2 w = rng_words(A, st, d, RNG_NORMAL, L);
+  if (L.lean && d == 0 && (st.flags & VBN_F_BM_FIRST)) {
+    const float u1 = (float)((w.x >> 8) + 1u) * (1.0f / 16777216.0f);
+    const float u2 = (float)(w.y >> 8) * (1.0f / 16777216.0f);
+    const float r = __builtin_sqrtf(-2.0f * __logf(u1));
+    L.bm_spare = r * __builtin_amdgcn_sinf(u2);
+    return r * __builtin_amdgcn_cosf(u2);
+  }
   return box_muller(w.x, w.y);
 }
 
@@ -1605,6 +1617,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
   L.mirror = (KM & 64) != 0;                         // host: wave_particles == 32
   L.lean = (KM & 128) != 0;                          // host: no noise, no state, not Gibbs
   L.noiseless = (KM & (128 | 256)) != 0;             // host: no injected draws
+  L.bm_spare = 0.f;
   const int wp = L.mirror ? 32 : WAVE;
   const int64_t p_raw = ((int64_t)blockIdx.x * nw + wave) * wp + (L.lane & (wp - 1));
   const bool valid = p_raw < total;

@@ -30,7 +30,7 @@ from .model import BNModel, CPDRecord
 KIND_ID = {"gaussian_nn": 0, "linear_gaussian": 1, "mdn": 2, "kde": 3, "softmax_nn": 4}
 ROLE_SKIP, ROLE_LATENT, ROLE_FIXED, ROLE_PARAMS, ROLE_SELECT, ROLE_COLLECT = 0, 1, 2, 3, 4, 5
 F_LOGP, F_ROOT, F_SHARED, F_STANDARDIZE, F_CLIP, F_F32L2, F_KDE_VALU = 1, 2, 4, 8, 16, 32, 64
-F_KEEP, F_LPRESET = 128, 256
+F_KEEP, F_LPRESET, F_BM_FIRST, F_BM_SECOND = 128, 256, 512, 1024
 ACT_ID = {"relu": 0, "tanh": 1, "gelu": 2, "elu": 3}
 WITHIN_ID = {"uniform": 0, "triangular": 1, "gaussian": 2}
 MODE_MCM, MODE_WEIGHTED, MODE_SAMPLE, MODE_GIBBS = 0, 1, 2, 3
@@ -529,6 +529,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         a = np.asarray(a, np.int32).reshape(-1) if len(a) else np.zeros(1, np.int32)
         return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
+    _pair_normals(steps)
     kind_mask = 0
     for n in order:
         if n in latent_s or n in logp_s or n in params_s:
@@ -545,6 +546,26 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         max_out=max_out, fixed_nodes=fixed_nodes, fixed_ld=max(c, 1), noise_nodes=noise_nodes,
         out_nodes=list(out_nodes), mode=mode, slot_of=slot_of, kind_mask=kind_mask,
         wbuf=int(steps[:, S_WBLK_LEN].max()) if len(order) else 0)
+
+
+def _pair_normals(steps: np.ndarray) -> None:
+    """Pair consecutive one-dimensional gaussian draws (csrc draw_normal, lean walks only): the
+    VBN_F_BM_FIRST step's Box-Muller pair gives r cos to itself and r sin, an independent N(0, 1),
+    to the next VBN_F_BM_SECOND step.  Pairs never mix draws shared across queries (F_SHARED
+    roots, Q5) with per-query ones, and one pair completes before the next starts (the kernel
+    keeps a single spare).  Injected draws and the other walk forms ignore the flags."""
+    gauss = (KIND_ID["gaussian_nn"], KIND_ID["linear_gaussian"])
+    pending = -1
+    for i in range(len(steps)):
+        r = steps[i]
+        if r[S_ROLE] != ROLE_LATENT or r[S_KIND] not in gauss or r[S_OUTDIM] != 1:
+            continue
+        if pending >= 0 and (steps[pending][S_FLAGS] & F_SHARED) == (r[S_FLAGS] & F_SHARED):
+            steps[pending][S_FLAGS] |= F_BM_FIRST
+            r[S_FLAGS] |= F_BM_SECOND
+            pending = -1
+        else:
+            pending = i
 
 
 @dataclass
@@ -607,6 +628,7 @@ def build_gibbs_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Seque
     r[S_FLAGS] = 0
     table.append(r)
     tab = np.ascontiguousarray(np.stack(table))
+    tab[:, S_FLAGS] &= ~(F_BM_FIRST | F_BM_SECOND)                          # walk-only pairing
     sel = (tab[:, S_ROLE] == ROLE_SELECT) | (tab[:, S_ROLE] == ROLE_COLLECT)
     tab[sel, S_WBLK_OFF] = 0                                              # no MLP on these rows
     tab[sel, S_WBLK_LEN] = 0
