@@ -85,7 +85,7 @@ enum vbn_role {
 #define VBN_F_KDE_VALU 64   /* kde: pairwise distances on packed VALU (else the 16x16x4 f32 MFMA tile) */
 #define VBN_F_KEEP 128      /* fixed role: the value is already in the node's slot (Gibbs)      */
 #define VBN_F_LPRESET 256   /* reset the particle's log-prob accumulator before this step       */
-#define VBN_F_BM_FIRST 512  /* production draw: this step's Box-Muller pair also yields the next */
+#define VBN_F_BM_FIRST 512  /* lean walks: this step's Box-Muller pair also yields the next     */
                             /* VBN_F_BM_SECOND step's dim-0 normal (r sin; this step takes r cos) */
 #define VBN_F_BM_SECOND 1024
 

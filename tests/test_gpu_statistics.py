@@ -12,8 +12,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _roots_model(n_roots=6):
-    """n independent linear_gaussian roots and one child of the first two."""
+def _roots_model(n_roots=6, kinds=("linear_gaussian",)):
+    """n independent roots (kinds round-robin) and one linear_gaussian child of the first two."""
     from vectorizedbayesiannetwork_amd import VBN, synthetic
     from vectorizedbayesiannetwork_amd.model import random_init_model
     g = nx.DiGraph()
@@ -22,7 +22,9 @@ def _roots_model(n_roots=6):
     g.add_edge("r0", "c")
     g.add_edge("r1", "c")
     data = synthetic.sem_data(g, 2048, seed=0)
-    model = random_init_model(g, {n: "linear_gaussian" for n in g.nodes}, data, seed=0)
+    kind_of = {n: kinds[i % len(kinds)] for i, n in enumerate(roots)}
+    kind_of["c"] = "linear_gaussian"
+    model = random_init_model(g, kind_of, data, seed=0, overrides={"kde": {"max_points": 512}})
     return model, VBN.from_model(model, device="cuda"), roots
 
 
@@ -77,3 +79,25 @@ def test_paired_normals_leave_injected_noise_parity_alone():
         eps = noise[plan.noise_nodes.index(r), 1, 0, :, 0]
         ratio = (xs[r].reshape(-1) - loc) / eps
         assert torch.allclose(ratio, ratio[:1].expand_as(ratio), rtol=1e-4, atol=1e-5), r
+
+
+def test_paired_normals_across_kinds_stay_independent():
+    """Pairs also join mdn and kde draws (plan._pair_normals): roots of three kinds, sampled in
+    the lean walk, stay pairwise uncorrelated (values and squares)."""
+    from vectorizedbayesiannetwork_amd import engines as E
+    from vectorizedbayesiannetwork_amd.engines import AncestralSampler, Query
+    model, vbn, roots = _roots_model(6, kinds=("linear_gaussian", "mdn", "kde"))
+    n = 1 << 17
+    torch.manual_seed(2)
+    xs = AncestralSampler(n_samples=n).sample(vbn, Query(target=None, evidence={}, do={}), n_samples=n)
+    flags = E.LAST_LAUNCH["plan"].steps[:, 2].cpu().numpy()
+    assert (flags & 1024).sum() >= 2
+    z = {}
+    for r in roots:
+        x = xs[r].reshape(-1).double().cpu().numpy()
+        assert np.isfinite(x).all()
+        z[r] = (x - x.mean()) / x.std()
+    for i, a in enumerate(roots):
+        for b in roots[i + 1:]:
+            assert abs(float(np.corrcoef(z[a], z[b])[0, 1])) < 5 / math.sqrt(n), (a, b)
+            assert abs(float(np.corrcoef(z[a] ** 2, z[b] ** 2)[0, 1])) < 0.05, (a, b)   # heavy tails

@@ -382,7 +382,7 @@ def test_normal_pairs_are_consecutive_and_class_pure():
                                                     PackedModel, build_plan)
     g = synthetic.random_dag(20, seed=0)
     data = synthetic.sem_data(g, 512, seed=0)
-    kinds = synthetic.round_robin_kinds(g, ["gaussian_nn", "linear_gaussian", "mdn"])
+    kinds = synthetic.round_robin_kinds(g, ["gaussian_nn", "linear_gaussian", "mdn", "softmax_nn"])
     pk = PackedModel(random_init_model(g, kinds, data, seed=0), "cpu")
     topo = pk.model.topo
     ev = set(topo[3::5])
@@ -395,7 +395,7 @@ def test_normal_pairs_are_consecutive_and_class_pure():
         f = int(r[S_FLAGS])
         if f & (F_BM_FIRST | F_BM_SECOND):
             assert r[S_ROLE] == ROLE_LATENT and r[S_OUTDIM] == 1
-            assert r[S_KIND] in (KIND_ID["gaussian_nn"], KIND_ID["linear_gaussian"])
+            assert r[S_KIND] in (KIND_ID["gaussian_nn"], KIND_ID["linear_gaussian"], KIND_ID["mdn"], KIND_ID["kde"])
         if f & F_BM_FIRST:
             assert open_first is None
             open_first = f & F_SHARED

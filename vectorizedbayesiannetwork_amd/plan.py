@@ -549,12 +549,14 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
 
 
 def _pair_normals(steps: np.ndarray) -> None:
-    """Pair consecutive one-dimensional gaussian draws (csrc draw_normal, lean walks only): the
+    """Pair consecutive one-dimensional normal draws (csrc draw_normal, lean walks only): the
     VBN_F_BM_FIRST step's Box-Muller pair gives r cos to itself and r sin, an independent N(0, 1),
     to the next VBN_F_BM_SECOND step.  Pairs never mix draws shared across queries (F_SHARED
     roots, Q5) with per-query ones, and one pair completes before the next starts (the kernel
     keeps a single spare).  Injected draws and the other walk forms ignore the flags."""
-    gauss = (KIND_ID["gaussian_nn"], KIND_ID["linear_gaussian"])
+    # kinds whose LATENT step always draws exactly one dim-0 normal (softmax_nn draws one only
+    # in its gaussian within-bin mode, so it is left out)
+    gauss = (KIND_ID["gaussian_nn"], KIND_ID["linear_gaussian"], KIND_ID["mdn"], KIND_ID["kde"])
     pending = -1
     for i in range(len(steps)):
         r = steps[i]
