@@ -124,6 +124,7 @@ struct Lane {
   bool lean;     // no injected draws, no segment state, not Gibbs (kind-set bit 7): the
                  // kernel sets these from KM, so every inlined check on them folds away
   bool noiseless;  // no injected draws (lean, or kind-set bit 8: production Gibbs)
+  bool wq;       // every lane of the wave is in the same query (S a multiple of the wave's particles)
   mutable float bm_spare;  // lean walks: the r sin half of a VBN_F_BM_FIRST step's Box-Muller pair
 };
 
@@ -184,11 +185,23 @@ __device__ __forceinline__ float2 draw_uniforms(const vbn_walk_args& A, const vb
   return make_float2(u01(w.x), u01(w.y));
 }
 
+// Read-only buffers (parameter blob, slot lists, evidence) seen through the constant address
+// space: wave-uniform reads become scalar loads (s_load, lgkmcnt) instead of vector loads.
+typedef __attribute__((address_space(4))) const float cfloat;
+typedef __attribute__((address_space(4))) const int32_t cint;
+#define CP(p) ((cfloat*)(p))
+#define CI(p) ((cint*)(p))
+
 __device__ __forceinline__ float vread(const Lane& L, int slot) { return L.vals[slot * WAVE + L.lane]; }
 __device__ __forceinline__ void vwrite(const Lane& L, int slot, float v) { L.vals[slot * WAVE + L.lane] = v; }
 
 __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_step& st, int d,
                                              const Lane& L) {
+  if (!A.fixed_per_particle && L.wq) {               // one query per wave: a scalar load
+    const int64_t b = ((int64_t)__builtin_amdgcn_readfirstlane((int)(L.b >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)L.b);
+    return CP(A.fixed)[b * A.fixed_ld + st.fixed_col + d];
+  }
   const int64_t row = A.fixed_per_particle ? L.p : L.b;
   return A.fixed[row * A.fixed_ld + st.fixed_col + d];
 }
@@ -231,20 +244,23 @@ __device__ __forceinline__ float node_fixed(const vbn_walk_args& A, const vbn_st
 
 // layer-1 B operand of k-step t for group g: z[2t + half] of particle (c + 32 g); the
 // column beyond n_in (odd n_in) is 0.
+// The operands of both lane halves are read with wave-uniform addresses (scalar loads) and
+// selected per lane: a per-lane address would make them vector loads, whose vmcnt wait also
+// waits for the next step's weight-block DMA.
 template <bool STD, int NIN>
 __device__ __forceinline__ float l1_operand(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
                                             int t, int g) {
-  const float* __restrict__ P = L.P;
   const int half = L.lane >> 5;
   const int nin = NIN > 0 ? NIN : st.n_in;
   const int kk = 2 * t + half;
   const int ke = min(2 * t, nin - 1), ko = min(2 * t + 1, nin - 1);
-  const int slot = half ? L.ic[st.in_off + ko] : L.ic[st.in_off + ke];
+  const int se = CI(L.ic)[st.in_off + ke], so = CI(L.ic)[st.in_off + ko];
+  const int slot = half ? so : se;
   float z = L.vals[slot * WAVE + (L.lane & 31) + 32 * g];
   if (STD) {
-    const float m = half ? P[st.off_std + ko] : P[st.off_std + ke];
-    const float is = half ? P[st.off_std + nin + ko] : P[st.off_std + nin + ke];
-    z = (z - m) * is;
+    const cfloat* sp = CP(L.P) + st.off_std;
+    const float me = sp[ke], mo = sp[ko], ie = sp[nin + ke], io = sp[nin + ko];
+    z = (z - (half ? mo : me)) * (half ? io : ie);
   }
   return kk < nin ? z : 0.0f;
 }
@@ -549,7 +565,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
   const int D = st.out_dim;
   const bool latent = st.role == VBN_ROLE_LATENT;
   const bool want_lp = (st.flags & VBN_F_LOGP) != 0;
-  const float* t = P + st.off_tail;
+  const cfloat* t = CP(P + st.off_tail);
   if (st.flags & VBN_F_ROOT) {
     for (int d = 0; d < D; ++d) {
       const float loc = t[d], scale = t[D + d];
@@ -616,11 +632,11 @@ __device__ __forceinline__ void step_linear_gaussian(const vbn_walk_args& A, con
 #pragma clang fp contract(off)
   const float* __restrict__ P = L.P;
   const int D = st.out_dim, nin = st.n_in;
-  const float* t = P + st.off_tail;
-  const float* W = t;
-  const float* bias = t + D * nin;
-  const float* scale = bias + D;
-  const float* log_scale = scale + D;
+  const cfloat* t = CP(P + st.off_tail);
+  const cfloat* W = t;
+  const cfloat* bias = t + D * nin;
+  const cfloat* scale = bias + D;
+  const cfloat* log_scale = scale + D;
   const bool latent = st.role == VBN_ROLE_LATENT;
   float acc = 0.f;
   for (int d = 0; d < D; ++d) {
@@ -674,7 +690,7 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
 #pragma clang fp contract(off)
   const float* __restrict__ P = L.P;
   const int D = st.out_dim, K = st.k;
-  const float* t = P + st.off_tail;
+  const cfloat* t = CP(P + st.off_tail);
   const bool root = (st.flags & VBN_F_ROOT) != 0;
   const bool latent = st.role == VBN_ROLE_LATENT;
   const bool want_lp = (st.flags & VBN_F_LOGP) != 0;
@@ -762,10 +778,10 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
 #pragma clang fp contract(off)
   const float* __restrict__ P = L.P;
   const int D = st.out_dim, C = st.k;
-  const float* t = P + st.off_tail;
-  const float* edges = t;
-  const float* svals = t + D * (C + 1);
-  const float* cvals = svals + D * C;
+  const cfloat* t = CP(P + st.off_tail);
+  const cfloat* edges = t;
+  const cfloat* svals = t + D * (C + 1);
+  const cfloat* cvals = svals + D * C;
   const float wscale = cvals[D * C + 0];
   const float min_bw = cvals[D * C + 1];
   const float min_bw2 = cvals[D * C + 2];
@@ -791,7 +807,7 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
       return;
     }
     const bool disc = (st.aux1 >> d) & 1;
-    const float* e = edges + d * (C + 1);
+    const cfloat* e = edges + d * (C + 1);
     float x;
     int idx;
     if (latent) {
@@ -1341,7 +1357,7 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
   const float* __restrict__ P = L.P;
   const float* __restrict__ pts = P + st.off_pts;
   const int M = st.k, dp = DP >= 0 ? DP : st.aux0, stride = st.aux1, D = DY > 0 ? DY : st.out_dim;
-  const float* t = P + st.off_tail;
+  const cfloat* t = CP(P + st.off_tail);
   const float inv_sp = t[0], inv_sy = t[1], noise_scale = t[2], cy = t[3], log_n = t[4];
   const float c_p = t[5], c_y = t[6];
   const bool root = (st.flags & VBN_F_ROOT) != 0;
@@ -1578,8 +1594,15 @@ __device__ __forceinline__ void stage_block(const vbn_walk_args& A, const vbn_st
                                      (lds_void*)(dst + c * WBLK_CHUNK), 16, 0, 0);
 }
 
-// end of a step: this wave's LDS-DMA has landed, every wave of the workgroup is done with the
-// buffer the next step's prefetch overwrites
+// first step >= j that runs an MLP (has a weight block), or -1
+__device__ __forceinline__ int first_mlp(const vbn_step* __restrict__ steps, int j, int n) {
+  for (; j < n; ++j)
+    if (CI(steps)[j * (int)(sizeof(vbn_step) / 4) + (int)(offsetof(vbn_step, reserved) / 4) + 6] > 0) return j;
+  return -1;
+}
+
+// start of an MLP step: this wave's LDS-DMA of the step's block has landed, every wave of the
+// workgroup is done with the buffer the next MLP step's prefetch overwrites
 __device__ __forceinline__ void step_barrier() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #ifdef VBN_ABL_NOBAR
@@ -1619,6 +1642,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
   L.noiseless = (KM & (128 | 256)) != 0;             // host: no injected draws
   L.bm_spare = 0.f;
   const int wp = L.mirror ? 32 : WAVE;
+  L.wq = A.mode != VBN_MODE_GIBBS && (A.n_samples & (wp - 1)) == 0;
   const int64_t p_raw = ((int64_t)blockIdx.x * nw + wave) * wp + (L.lane & (wp - 1));
   const bool valid = p_raw < total;
   L.p = valid ? p_raw : total - 1;
@@ -1635,18 +1659,25 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
   }
   const int iters = (!L.lean && A.mode == VBN_MODE_GIBBS) ? A.gibbs_iters : 1;
   if constexpr (staged_kinds(KM)) {
+  // Only MLP steps (wblk_len > 0) touch the weight buffers, so only they synchronise: MLP step
+  // k waits for its block (DMA'd during MLP step k - 1), then, once every wave is past that
+  // barrier (so done with the other buffer), DMAs MLP step k + 1's block into it.  The DMA
+  // overlaps MLP step k and every root / evidence step up to k + 1.
   int par = 0;
-  if (A.n_steps > 0) stage_block(A, steps, params, wbuf, 0, 0, wave, nw, L.lane);
-  step_barrier();
+  int nxt = first_mlp(steps, 0, A.n_steps);
+  if (nxt >= 0) stage_block(A, steps, params, wbuf, nxt, 0, wave, nw, L.lane);
   for (int it = 0; it < iters; ++it) {
     L.iter = it;
     for (int i = 0; i < A.n_steps; ++i) {
-      const bool last = i + 1 == A.n_steps;
-      if (!last || it + 1 < iters) stage_block(A, steps, params, wbuf, last ? 0 : i + 1, par ^ 1, wave, nw, L.lane);
-      L.wb = wbuf + par * A.wbuf_floats;
+      if (i == nxt) {
+        step_barrier();
+        nxt = first_mlp(steps, i + 1, A.n_steps);
+        if (nxt < 0 && it + 1 < iters) nxt = first_mlp(steps, 0, A.n_steps);   // next sweep
+        if (nxt >= 0) stage_block(A, steps, params, wbuf, nxt, par ^ 1, wave, nw, L.lane);
+        L.wb = wbuf + par * A.wbuf_floats;
+        par ^= 1;
+      }
       walk_step<KM>(A, steps[i], L, lp);
-      step_barrier();
-      par ^= 1;
     }
   }
   } else {
