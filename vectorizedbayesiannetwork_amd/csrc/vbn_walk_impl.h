@@ -713,14 +713,18 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
     for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, scr[k * WAVE + lane]);
     lsum = 0.f;
     for (int k = 0; k < K; ++k) lsum += __expf(scr[k * WAVE + lane] - lmax);
+    // pi_k computed once per particle into the logit rows (the inverse CDF and the log-prob
+    // read pi_k repeatedly; same operations, so the same values)
     psum = 0.f;
-    for (int k = 0; k < K; ++k) psum += fmaxf(__expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f);
+    for (int k = 0; k < K; ++k) {
+      const float p = fmaxf(__expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f);
+      scr[k * WAVE + lane] = p;
+      psum += p;
+    }
     psum = fmaxf(psum, 1e-12f);
+    for (int k = 0; k < K; ++k) scr[k * WAVE + lane] = scr[k * WAVE + lane] / psum;
   }
-  auto pi_k = [&](int k) -> float {
-    if (root) return t[k];
-    return fmaxf(__expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f) / psum;
-  };
+  auto pi_k = [&](int k) -> float { return root ? t[k] : scr[k * WAVE + lane]; };
   auto loc_kd = [&](int k, int d) -> float {
     return root ? t[2 * K + k * D + d] : scr[(K + k * 2 * D + d) * WAVE + lane];
   };
@@ -812,7 +816,14 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
     int idx;
     if (latent) {
       const float2 uu = d == 0 ? uu0 : draw_uniforms(A, st, d, L);
-      idx = inv_cdf(C, uu.x, [&](int c) { return __expf(logit(c) - m) / se; });
+      if (!root && !(st.flags & VBN_F_LOGP)) {
+        // the logits are not read again: the class probabilities replace them, computed once
+        // (the inverse CDF reads each twice; same operations, so the same values)
+        for (int c = 0; c < C; ++c) L.scr[(d * C + c) * WAVE + lane] = __expf(logit(c) - m) / se;
+        idx = inv_cdf(C, uu.x, [&](int c) { return L.scr[(d * C + c) * WAVE + lane]; });
+      } else {
+        idx = inv_cdf(C, uu.x, [&](int c) { return __expf(logit(c) - m) / se; });
+      }
       const float left = e[idx];
       const float right = e[idx + 1 < C ? idx + 1 : C];
       const float width = fmaxf(right - left, min_bw);
