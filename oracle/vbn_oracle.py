@@ -547,6 +547,15 @@ def _fixed(evidence, do, clamp=False):
     return vals
 
 
+def _begin_node(draws, node: str, query: Optional[int] = None) -> None:
+    """Tell a node-aware draw provider which node (and, for IS's per-query loop, which query)
+    the next draws belong to (tests/philox_draws.py replays the HIP walk's Philox streams
+    this way); TorchDraws / ReplayDraws ignore it, so the call order is unchanged."""
+    hook = getattr(draws, "begin_node", None)
+    if hook is not None:
+        hook(node, query)
+
+
 def _gather_parents(model, node, particles, cols):
     ps = model.parents[node]
     if not ps:
@@ -568,6 +577,7 @@ def monte_carlo_marginalization(model: BNModel, target: str, evidence: Dict, do:
         if target in fixed:
             xs = fixed[target].unsqueeze(1).expand(b, n, -1)
         else:
+            _begin_node(draws, target)
             xs = cpd_sample(rec, pt, n, draws)
         return torch.exp(cpd_log_prob(rec, xs, pt)), xs
     cols, total = _layout(model)
@@ -576,6 +586,7 @@ def monte_carlo_marginalization(model: BNModel, target: str, evidence: Dict, do:
         if node in fixed:
             particles[..., cols[node]] = fixed[node].unsqueeze(1).expand(b, n, -1)
             continue
+        _begin_node(draws, node)
         particles[..., cols[node]] = cpd_sample(model.cpds[node], _gather_parents(model, node, particles, cols), n, draws)
     xs = particles[..., cols[target]]
     lp = cpd_log_prob(rec, xs, _gather_parents(model, target, particles, cols))   # 80-91
@@ -600,10 +611,12 @@ def _walk_weighted(model, evidence, do, n, draws, clamp, per_query):
         if per_query and b > 1:                       # importance_sampling.py:37-54
             parts = []
             for i in range(b):
+                _begin_node(draws, node, i)
                 si = cpd_sample(rec, None if pt is None else pt[i:i + 1], n, draws)
                 parts.append(si.unsqueeze(0) if si.dim() == 2 else si)
             particles[..., cols[node]] = torch.cat(parts, dim=0)
         else:
+            _begin_node(draws, node)
             particles[..., cols[node]] = cpd_sample(rec, pt, n, draws)
     return particles, log_w, cols
 
@@ -644,6 +657,7 @@ def ancestral(model: BNModel, target: Optional[str], evidence: Dict, do: Dict, n
         if node in fixed:
             particles[..., cols[node]] = fixed[node].unsqueeze(1).expand(b, n, -1)
             continue
+        _begin_node(draws, node)
         particles[..., cols[node]] = cpd_sample(model.cpds[node], _gather_parents(model, node, particles, cols), n, draws)
     if target:
         return particles[..., cols[target]]

@@ -203,7 +203,8 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
         noise_b = int(noise.shape[2])
         if noise.shape[3] != n or noise.shape[4] != pk.dmax:
             raise ValueError(f"noise must be [n_latent, 2, B|1, {n}, {pk.dmax}]")
-    LAST_LAUNCH.update(pk=pk, plan=plan, fixed=fixed, b=b, n=n, fixed_per_particle=fixed_per_particle)
+    LAST_LAUNCH.update(pk=pk, plan=plan, fixed=fixed, b=b, n=n, fixed_per_particle=fixed_per_particle,
+                       noise=noise, state=state, seed=seed, offset=offset)
     args = (plan.steps, plan.in_cols, pk.params, fixed, noise, plan.out_cols, b, n,
             plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
             len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
