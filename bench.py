@@ -4,15 +4,19 @@
 A step = one ``infer_posterior`` call over one batch of synthetic queries:
 default workload cfg2 = 32-node random DAG, gaussian_nn CPDs (random-init weights of the
 reference architecture, data-derived standardisation), 4096 queries x 1024 samples per GPU,
-monte_carlo_marginalization.  With N GPUs every rank runs its own 4096-query shard (weak
-scaling, global query index feeds the RNG); there is no data-path collective.
+monte_carlo_marginalization.  Every N runs the same path: the global batch (4096 x N
+queries) goes through ``ShardedEngine(engine, gather=True, overlap=True)`` -- each rank walks
+its contiguous 4096-query shard (weak scaling; the global query index keys the RNG) and the
+pdf / samples are gathered on rank 0 with one RCCL gather over xGMI per step, issued
+asynchronously so it overlaps the next step's walk (N = 1: no collective).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|anchor64]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg4|cfg5|anchor64|...]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Rank 0 prints one JSON line.  ``roofline`` prices the dominant kernel (vbn_walk_kernel) with
 HIP events on the stream it runs on; ``cpu_baseline`` times the CPU oracle (the reference's
-torch op sequence, oracle/vbn_oracle.py) on a bounded sample on this host's cores.
+torch op sequence, oracle/vbn_oracle.py) on a bounded sample on this host's cores, in a
+fresh child process with the tuned glibc allocator settings of BASELINE.md.
 """
 from __future__ import annotations
 
@@ -44,22 +48,29 @@ HBM_PEAK_GBS = 8000.0
 EXP_PEAK_T = 8 * 1024 * 2.4e9 / 1e12
 
 
-def build_workload(cfg_name: str, device: str, rank: int):
+def build_model(cfg_name: str):
+    """The synthetic model of ``cfg_name``: random DAG, SEM data, random-init
+    CPDs of the reference architectures; returns (cfg, model, target, evidence nodes)."""
     cfg = dict(synthetic.CONFIGS[cfg_name])
     g = synthetic.random_dag(cfg["n_nodes"], seed=0)
     data = synthetic.sem_data(g, cfg.get("rows", 2048), seed=0)
     kinds = synthetic.round_robin_kinds(g, cfg["kinds"])
     overrides = {"kde": {"max_points": cfg["kde_max_points"]}} if "kde_max_points" in cfg else None
     model = random_init_model(g, kinds, data, seed=0, overrides=overrides)
-    vbn = VBN.from_model(model, device=device)
     target, ev_nodes = synthetic.default_query_nodes(g, seed=1)
-    B, S = cfg["B"], cfg["S"]
-    # on-manifold evidence: B rows of the model's own ancestral draw (seed 2 + rank)
-    torch.manual_seed(2 + rank)
+    return cfg, model, target, ev_nodes
+
+
+def build_workload(cfg_name: str, device: str, world: int = 1):
+    """Model on ``device`` + the global query of ``world`` x B queries (identical on every
+    rank): on-manifold evidence = B rows of the model's own ancestral draw (seed 2)."""
+    cfg, model, target, ev_nodes = build_model(cfg_name)
+    vbn = VBN.from_model(model, device=device)
+    B = cfg["B"] * world
+    torch.manual_seed(2)
     joint = AncestralSampler(n_samples=B).sample(vbn, Query(target=None, evidence={}, do={}), n_samples=B)
     evidence = {n: joint[n][0].contiguous() for n in ev_nodes}
-    query = {"target": target, "evidence": evidence}
-    return cfg, g, model, vbn, query
+    return cfg, model, vbn, {"target": target, "evidence": evidence}
 
 
 def mlp_flops_per_particle(model, plan):
@@ -97,45 +108,82 @@ def kde_exps_per_particle(model, plan) -> float:
     return exps
 
 
-def cpu_baseline(cfg, model, query, n_queries: int, reps: int = 3):
-    """Oracle (reference op sequence, TorchDraws = the reference's RNG calls) on host cores."""
+CPU_ENV = {"MALLOC_MMAP_MAX_": "0", "MALLOC_TRIM_THRESHOLD_": "1000000000000"}
+
+
+def cpu_threads() -> int:
+    """Host cores this process may use: the CPU affinity set, capped by OMP_NUM_THREADS when
+    the launcher sets it (the GPU box grants one GPU's share of a larger host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else max(1, n)
+
+
+def cpu_baseline_child(cfg_name: str, n_queries: int, reps: int):
+    """Runs in a fresh child process (tuned glibc env, every granted core): the oracle (the
+    reference's op sequence and RNG calls, TorchDraws) on ``n_queries`` queries of the same
+    workload; 1 warm-up, median of ``reps``."""
     from oracle import vbn_oracle as O
-    threads = torch.get_num_threads()
-    ev = {k: v[:n_queries].cpu() for k, v in query["evidence"].items()}
-    S = cfg["S"]
-    eng = cfg["engine"]
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+    cfg, model, target, ev_nodes = build_model(cfg_name)
+    torch.manual_seed(2)                          # on-manifold evidence, as the GPU leg
+    joint = O.ancestral(model, None, {}, {}, n_queries, O.TorchDraws())
+    ev = {n: joint[n][0].contiguous() for n in ev_nodes}
+    query = {"target": target}
+    S, eng = cfg["S"], cfg["engine"]
+    fallbacks = []
 
     def one():
         with torch.no_grad():
             if eng == "monte_carlo_marginalization":
                 O.monte_carlo_marginalization(model, query["target"], ev, {}, S, O.TorchDraws())
             else:
-                O.importance_sampling(model, query["target"], ev, {}, S, O.TorchDraws())
+                fallbacks.append(bool(O.importance_sampling(model, query["target"], ev, {}, S, O.TorchDraws())[3]))
 
-    if reps > 1:
-        one()
+    one()
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
         one()
         ts.append(time.perf_counter() - t0)
     med = statistics.median(ts)
-    return {"value": n_queries / med, "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"{n_queries} queries x {S} samples, median of {reps}"
-                      f"{' after 1 warm-up' if reps > 1 else ''}, "
-                      f"torch CPU {threads} threads, no_grad"}
+    env = " ".join(f"{k}={os.environ.get(k, '')}" for k in CPU_ENV)
+    out = {"value": n_queries / med, "unit": "queries/s", "cores": threads, "kind": "port",
+           "sample": f"{n_queries} queries x {S} samples of {cfg_name}, median of {reps} after 1 warm-up, "
+                     f"torch CPU {threads} threads (affinity {len(os.sched_getaffinity(0))}, "
+                     f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}), no_grad, fresh process, {env}",
+           "seconds": [round(t, 4) for t in ts]}
+    if fallbacks:
+        out["is_fallback"] = any(fallbacks)
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline(cfg_name: str, n_queries: int, reps: int = 5):
+    """Start :func:`cpu_baseline_child` as a fresh process (never an exec of this one)."""
+    import subprocess
+    env = dict(os.environ, **CPU_ENV)
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", cfg_name,
+           "--cpu-queries", str(n_queries), "--cpu-reps", str(reps)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline child failed ({r.returncode}): {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def load_traffic(cfg_name: str):
-    """Per-launch HBM bytes of vbn_walk_kernel from the committed PMC summary (profiles/)."""
-    paths = sorted(glob.glob(os.path.join(REPO, "profiles", f"*{cfg_name}*pmc*.json")))
+    """Per-launch HBM bytes of vbn_walk_kernel from the newest committed rocprofv3 PMC summary
+    of this workload (profiles/r*_<cfg>_pmc.json; PMC counters cannot be read from inside the
+    timed process).  Returns (bytes or None, source path)."""
+    paths = glob.glob(os.path.join(REPO, "profiles", f"r*_{cfg_name}_pmc.json"))
+    paths.sort(key=lambda p: os.path.basename(p))
     if not paths:
-        return None
+        return None, None
     try:
         with open(paths[-1]) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            return json.load(f).get("hbm_bytes_per_launch"), os.path.relpath(paths[-1], REPO)
     except Exception:
-        return None
+        return None, None
 
 
 KT_UNTIMED, KT_TIMED = 20, 10     # roofline kernel timing: untimed launches, then timed ones
@@ -149,31 +197,48 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-queries", type=int, default=0)
+    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-gather", action="store_true", help="shards only (no RCCL gather of the outputs)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--prune-barren", action="store_true")
     ap.add_argument("--exact-f32", action="store_true", help="hidden layer on the exact f32 MFMA chain")
     ap.add_argument("--kde-valu", action="store_true", help="KDE distances on packed VALU (default: 16x16x4 f32 MFMA tile)")
     args = ap.parse_args()
+    if args.cpu_baseline_child:                       # fresh process, never touches the GPU
+        cpu_baseline_child(args.config, args.cpu_queries, args.cpu_reps)
+        return
 
+    from vectorizedbayesiannetwork_amd.distributed import ShardedEngine
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
     if dist:
         import torch.distributed as tdist
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:                                         # rehearsal: ranks share the visible GPUs
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            tdist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     device = f"cuda:{local}"
 
-    cfg, g, model, vbn, query = build_workload(args.config, device, rank)
-    B, S = cfg["B"], cfg["S"]
+    cfg, model, vbn, query = build_workload(args.config, device, world)
+    B, S = cfg["B"], cfg["S"]                         # B = queries per GPU
     extra = {"n_particles": S} if cfg["engine"] == "rao_blackwellized_marginalization" else {}
-    vbn.set_inference_method(cfg["engine"], n_samples=S, q_base=rank * B,
-                             prune_barren=args.prune_barren, exact_f32=args.exact_f32, kde_valu=args.kde_valu,
-                             **extra)
-    if cfg["engine"] == "importance_sampling":
-        vbn._inference._lw.q_base = rank * B
+    vbn.set_inference_method(cfg["engine"], n_samples=S, prune_barren=args.prune_barren,
+                             exact_f32=args.exact_f32, kde_valu=args.kde_valu, **extra)
+    engine = vbn._inference
+    gather = not args.no_gather
+    # every N the same path: shard the global batch, gather pdf / samples on rank 0 (async,
+    # overlapping the next step's walk); N = 1 is the trivial shard with no collective
+    sharded = ShardedEngine(engine, gather=gather, overlap=True)
+    vbn._inference = sharded
 
     def barrier():
         if dist:
@@ -185,6 +250,7 @@ def main():
     # the timed region (the first ~25 walks after idle run up to 17 % slower)
     from vectorizedbayesiannetwork_amd import engines as E
     vbn.infer_posterior(query)                # builds the plan of the timed steps
+    sharded.wait()
     torch.cuda.synchronize()
     last = dict(E.LAST_LAUNCH)
     pk, plan, fixed = last["pk"], last["plan"], last["fixed"]
@@ -209,31 +275,39 @@ def main():
 
     for _ in range(args.warmup):
         vbn.infer_posterior(query)
+    sharded.wait()
     torch.cuda.synchronize()
 
-    # timed region: exactly K steps, barrier + synchronize on both sides
+    # timed region: exactly K steps, barrier + synchronize on both sides (the synchronize
+    # also waits for the last step's gather on RCCL's stream)
+    fallbacks = []
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pdf, samples = vbn.infer_posterior(query)
+        if hasattr(engine, "_last_fallback"):
+            fallbacks.append(bool(engine._last_fallback))
+    sharded.wait()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=device if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / args.steps
     value = world * B * args.steps / elapsed
+    if rank == 0 and gather:
+        assert pdf is not None and pdf.shape[0] == world * B, "rank 0 must hold the gathered batch"
 
     f32_fl, hid_fl = mlp_flops_per_particle(model, plan)
     f32_fl, hid_fl = f32_fl * B * S, hid_fl * B * S
     flops = f32_fl + hid_fl
-    exact = bool(getattr(vbn._inference, "exact_f32", False))
+    exact = bool(getattr(engine, "exact_f32", False))
     hid_peak = FP32_PEAK_TFLOPS if exact else F16_PEAK_TFLOPS / SPLIT_PASSES
     exps = kde_exps_per_particle(model, plan) * B * S
-    traffic = load_traffic(args.config)
+    traffic, traffic_src = load_traffic(args.config)
     kern_s = kern_ms * 1e-3
     if exps > 0.1 * flops / 64:
         # KDE: one exp per (particle, point) kernel weight; the bound is the v_exp_f32 issue rate
@@ -255,7 +329,10 @@ def main():
                 "peak_basis": f"f32 FLOPs at {FP32_PEAK_TFLOPS} TF, hidden-layer FLOPs at {hid_peak:.1f} TF",
                 "f32_equiv_frac_of_fp32_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
                 "launches_timed": reps, "launches_untimed_before": untimed + 1}
+    roof["traffic_source"] = traffic_src
 
+    par = f"query-sharded dp{world}" + (" + one RCCL gather of pdf/samples to rank 0 per step (async, "
+                                        "overlapping the next walk)" if gather and dist else "")
     out = {
         "metric": "posterior queries/sec (infer_posterior, n_samples=1024) at 1/2/4/8 MI355X",
         "value": round(value, 2),
@@ -271,16 +348,19 @@ def main():
         "data": "synthetic (SURVEY §8d DAG/SEM/query generator; random-init CPD weights)",
         "config": {"workload": f"{args.config}: {cfg['name']}", "queries_per_gpu": B, "global_batch": B * world,
                    "n_samples": S, "n_nodes": cfg["n_nodes"], "engine": cfg["engine"],
-                   "parallelism": f"query-sharded dp{world}", "prune_barren": args.prune_barren,
+                   "parallelism": par, "gather": gather and dist, "prune_barren": args.prune_barren,
                    "exact_f32": args.exact_f32, "kde_distances": "valu" if args.kde_valu else "mfma"},
         "roofline": roof,
     }
+    if fallbacks:
+        out["config"]["is_fallback_steps"] = sum(fallbacks)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         kde = "kde" in cfg["kinds"]
         nq = args.cpu_queries or (1024 if cfg["engine"] == "monte_carlo_marginalization" and cfg["n_nodes"] <= 64
                                   and not kde else (1 if kde else 8))
-        print(f"cpu baseline: {nq} queries on the host ...", file=sys.stderr, flush=True)
-        out["cpu_baseline"] = cpu_baseline(cfg, model, query, nq, reps=1 if kde else 3)
+        reps_cpu = 1 if kde else args.cpu_reps
+        print(f"cpu baseline: {nq} queries in a child process ...", file=sys.stderr, flush=True)
+        out["cpu_baseline"] = cpu_baseline(args.config, nq, reps_cpu)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -41,34 +41,59 @@ class StubEngine:
         return pdf, (pdf.unsqueeze(-1) + ev.unsqueeze(1))
 
 
+def _expected_seed(calls: int = 1) -> int:
+    """The seed of call ``calls`` of a ShardedEngine: rank 0's first torch draw (seeded 123),
+    broadcast once, seeds the rank-replicated stream the per-call seeds come from."""
+    from vectorizedbayesiannetwork_amd.distributed import seed_stream
+    torch.manual_seed(123)
+    gen = seed_stream(int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item()))
+    for _ in range(calls):
+        seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, generator=gen).item())
+    return seed
+
+
 def _rendezvous():
     """A fresh file:// rendezvous for one world (no TCP port to race for between tests)."""
     return "file://" + os.path.join(tempfile.mkdtemp(prefix="vbn_gloo_"), "store")
 
 
-def _worker(rank, world, init, ev, out_q):
+def _worker(rank, world, init, ev, out_q, calls=1, overlap=False):
     dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     try:
         torch.manual_seed(123 + rank)                 # ranks disagree; the seed is broadcast
-        eng = ShardedEngine(StubEngine(), gather=True)
-        pdf, xs = eng.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}))
+        eng = ShardedEngine(StubEngine(), gather=True, overlap=overlap)
+        for _ in range(calls):                        # later calls: no collective for the seed
+            pdf, xs = eng.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}))
+        eng.wait()
         out_q.put((rank, None if pdf is None else pdf.clone(), None if xs is None else xs.clone(),
                    eng.engine.last_fallback))
     finally:
         dist.destroy_process_group()
 
 
-def _run(ev, world=2):
+def _run(ev, world=2, calls=1, overlap=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     init = _rendezvous()
-    procs = [ctx.Process(target=_worker, args=(r, world, init, ev, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, init, ev, q, calls, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
     return sorted(res, key=lambda r: r[0])
+
+
+@pytest.mark.parametrize("ragged", [False, True])
+def test_gloo_world2_overlapped_gather_third_call(ragged):
+    """overlap=True (async gather, results valid after wait()) on the third call: seeds come
+    from the replicated stream, equal shards gather straight into the batch buffer."""
+    ev = torch.linspace(-1, 1, 7 if ragged else 8).unsqueeze(1)
+    (r0, pdf, xs, fb0), (r1, pdf1, xs1, fb1) = _run(ev, calls=3, overlap=True)
+    assert pdf1 is None and xs1 is None
+    rpdf, rxs = StubEngine().infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}),
+                                             seed=_expected_seed(3))
+    assert torch.equal(pdf, rpdf) and torch.equal(xs, rxs)
 
 
 def test_shard_bounds_cover_batch():
@@ -92,9 +117,7 @@ def test_gloo_world2_matches_single_process(hot):
     (r0, pdf, xs, fb0), (r1, pdf1, xs1, fb1) = res
     assert pdf1 is None and xs1 is None                # gathered on rank 0 only
     assert fb0 == fb1 == hot
-    # single-process reference with the seed rank 0 broadcast
-    torch.manual_seed(123)
-    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    seed = _expected_seed()
     ref = StubEngine()
     rpdf, rxs = ref.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}), seed=seed)
     assert torch.equal(pdf, rpdf)
@@ -141,8 +164,7 @@ def test_gloo_world2_sharded_chains_match_single_process():
         p.join(timeout=60)
     (_, xs), (_, xs1) = res
     assert xs1 is None
-    torch.manual_seed(123)
-    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    seed = _expected_seed()
     ref = StubChainSampler().sample(None, Query(target="y", evidence={"x": ev}, do={}), 5, seed=seed)
     assert torch.equal(xs, ref)
 

@@ -28,6 +28,7 @@ import torch
 
 from oracle import vbn_oracle as O
 from philox_draws import PhiloxDraws
+from workloads import synthetic_workload
 
 pytestmark = pytest.mark.gpu
 
@@ -39,20 +40,7 @@ B_PARITY, S_PARITY = 8, 1024
 
 
 def _workload(cfg_name: str, n_queries: int):
-    from vectorizedbayesiannetwork_amd import VBN, synthetic
-    from vectorizedbayesiannetwork_amd.model import random_init_model
-    cfg = synthetic.CONFIGS[cfg_name]
-    g = synthetic.random_dag(cfg["n_nodes"], seed=0)
-    data = synthetic.sem_data(g, cfg.get("rows", 2048), seed=0)
-    kinds = synthetic.round_robin_kinds(g, cfg["kinds"])
-    overrides = {"kde": {"max_points": cfg["kde_max_points"]}} if "kde_max_points" in cfg else None
-    model = random_init_model(g, kinds, data, seed=0, overrides=overrides)
-    vbn = VBN.from_model(model, device="cuda")
-    target, ev_nodes = synthetic.default_query_nodes(g, seed=1)
-    torch.manual_seed(2)                         # on-manifold evidence: the model's own draw
-    joint = O.ancestral(model, None, {}, {}, n_queries, O.TorchDraws())
-    evidence = {n: joint[n][0].clone() for n in ev_nodes}
-    return model, vbn, target, evidence
+    return synthetic_workload(cfg_name, n_queries, "cuda")
 
 
 def _provider(plan, pk, seed, b, s, offset=0):
@@ -135,7 +123,7 @@ def test_lean_weighted_walk_matches_oracle(cfg_name, engine):
 @pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3"])
 def test_lean_is_engine_matches_oracle(cfg_name):
     """The whole IS call: walk + wave-reduced softmax / ESS + batch-global fallback decision;
-    weights compared on the queries with no categorical near-tie."""
+    a query may differ only if one of its particles had a categorical near-tie."""
     from vectorizedbayesiannetwork_amd import engines as E
     from vectorizedbayesiannetwork_amd.engines import ImportanceSampling, Query
     model, vbn, target, ev = _workload(cfg_name, B_PARITY)
@@ -149,13 +137,13 @@ def test_lean_is_engine_matches_oracle(cfg_name):
     draws = _provider(last["plan"], last["pk"], seed, B_PARITY, S_PARITY)
     rw, rxs, ress, rfb = O.importance_sampling(model, target, ev, {}, S_PARITY, draws)
     assert rfb is False
-    clean = ~(draws.min_margin() < TIE).any(axis=1)
-    assert clean.sum() >= B_PARITY // 2
-    cq = torch.from_numpy(clean)
-    bad_w, ew = _mismatch(w.cpu()[cq], rw[cq], P_ATOL, P_RTOL)
-    bad_e, ee = _mismatch(eng._last_ess.cpu()[cq].view(-1, 1), ress[cq].view(-1, 1), 1e-5, P_RTOL)
-    print(f"{cfg_name} IS engine: {int(clean.sum())} clean queries, max |dw| {ew:.3g}, max |dESS| {ee:.3g}")
-    assert not bad_w.any() and not bad_e.any()
+    tie_q = (draws.min_margin() < TIE).any(axis=1)
+    bad_w, ew = _mismatch(w.cpu(), rw, P_ATOL, P_RTOL)
+    bad_e, ee = _mismatch(eng._last_ess.cpu().view(-1, 1), ress.view(-1, 1), 1e-5, P_RTOL)
+    bad_q = bad_w.any(axis=1) | bad_e[:, 0]
+    print(f"{cfg_name} IS engine: {int(bad_q.sum())} differing queries of {B_PARITY} "
+          f"({int(tie_q.sum())} with a categorical near-tie), max |dw| {ew:.3g}, max |dESS| {ee:.3g}")
+    assert not (bad_q & ~tie_q).any(), "a query differs without a categorical near-tie"
 
 
 @pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3"])

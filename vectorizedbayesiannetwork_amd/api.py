@@ -202,6 +202,8 @@ class VBN:
             raise RuntimeError("Call set_inference_method(...) before infer_posterior().")
         q = self._normalize_query(query)
         pdf, samples = self._inference.infer_posterior(self, q, **kwargs)
+        if pdf is None:                     # ShardedEngine(gather=True) on a rank other than dst
+            return None, None
         return pdf.detach(), samples.detach()
 
     def sample(self, query, n_samples: int = 200, **kwargs):

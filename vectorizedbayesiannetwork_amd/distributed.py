@@ -4,14 +4,21 @@ Queries are independent, so the batch is split into contiguous shards and each r
 its own shard with no data-path collective.  Two things keep the result
 identical to a single-GPU run of the whole batch:
 
-* every rank uses the same RNG seed (broadcast from rank 0 once per call) and its shard's
-  global query offset (``q_base``) keys the per-query Philox streams; root-node draws that
-  the reference shares across the batch (Q5) are keyed without the query and so agree;
+* every rank uses the same RNG seed and its shard's global query offset (``q_base``) keys the
+  per-query Philox streams; root-node draws that the reference shares across the batch (Q5)
+  are keyed without the query and so agree.  The seed of each call comes from a
+  rank-replicated generator seeded once from rank 0's torch generator (one 8-byte broadcast
+  on the first call), so later calls need no collective and no host sync;
 * the importance-sampling fallback stays batch-global (Q6): the per-rank "any ESS below
   threshold" flag is all-reduced with MAX (a 4-byte RCCL all-reduce) before deciding.
 
-``gather=True`` additionally collects pdf/samples on ``dst`` (RCCL gather over xGMI).
-The same code runs on ``gloo`` for CPU tests (with a CPU stand-in engine).
+``gather=True`` additionally collects pdf/samples on ``dst`` (RCCL gather over xGMI: every
+peer sends its shard over its own link to ``dst``, straight into one preallocated
+``[world, shard, ...]`` buffer whose view is the batch).  ``overlap=True`` issues the gather
+asynchronously so that it runs on RCCL's stream while the next call's walk computes; the
+returned tensors are then valid after :meth:`ShardedEngine.wait` (as with any
+``async_op`` collective).  The same code runs on ``gloo`` (CPU collectives) for the
+multi-process tests.
 """
 from __future__ import annotations
 
@@ -22,7 +29,12 @@ import torch.distributed as dist
 
 from .engines import Query, infer_batch_size
 
-__all__ = ["shard_bounds", "shard_query", "ShardedEngine"]
+__all__ = ["shard_bounds", "shard_query", "ShardedEngine", "seed_stream"]
+
+
+def seed_stream(base: int) -> torch.Generator:
+    """The rank-replicated generator the per-call seeds of a :class:`ShardedEngine` come from."""
+    return torch.Generator().manual_seed(int(base))
 
 
 def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -80,11 +92,15 @@ def _world(group) -> Tuple[int, int]:
 class ShardedEngine:
     """Wrap an engine (``infer_posterior`` or ``sample``) for query-sharded multi-GPU runs."""
 
-    def __init__(self, engine, group=None, gather: bool = False, dst: int = 0):
+    def __init__(self, engine, group=None, gather: bool = False, dst: int = 0, overlap: bool = False):
         self.engine = engine
         self.group = group
         self.gather = bool(gather)
         self.dst = int(dst)
+        self.overlap = bool(overlap)
+        self._gen: Optional[torch.Generator] = None
+        self._pending = []
+        self.last_seed: Optional[int] = None
 
     def _device(self):
         backend = dist.get_backend(self.group) if dist.is_initialized() else "gloo"
@@ -95,12 +111,21 @@ class ShardedEngine:
     def _shared_seed(self, kwargs) -> int:
         if kwargs.get("seed") is not None:
             return int(kwargs["seed"])
-        rank, world = _world(self.group)
-        s = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
-        if world > 1:
-            s = s.to(self._device())
-            dist.broadcast(s, src=0, group=self.group)
-        return int(s.item())
+        if self._gen is None:                        # once: rank 0's draw, broadcast
+            rank, world = _world(self.group)
+            s = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
+            if world > 1:
+                s = s.to(self._device())
+                dist.broadcast(s, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0,
+                               group=self.group)
+            self._gen = seed_stream(int(s.item()))
+        return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, generator=self._gen).item())
+
+    def wait(self) -> None:
+        """Order the current stream after every pending (``overlap=True``) gather."""
+        for w in self._pending:
+            w.wait()
+        self._pending.clear()
 
     def _flag_reducer(self):
         rank, world = _world(self.group)
@@ -127,19 +152,29 @@ class ShardedEngine:
             return t
         dev = self._device()
         q_max = -(-n_total // world)
-        pad = torch.zeros((q_max,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
-        pad[: t.shape[0]] = t.to(dev)
-        parts = [torch.empty_like(pad) for _ in range(world)] if rank == self.dst else None
-        dist.gather(pad, parts, dst=self.dst, group=self.group)
+        src = t.to(dev).contiguous()
+        if src.shape[0] != q_max:                     # ragged last shards: pad to q_max rows
+            pad = torch.zeros((q_max,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+            pad[: src.shape[0]] = src
+            src = pad
+        out = parts = None
+        if rank == self.dst:
+            out = torch.empty((world, q_max) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+            parts = list(out.unbind(0))
+        work = dist.gather(src, parts, dst=self.dst, group=self.group, async_op=self.overlap)
+        if self.overlap:
+            self._pending.append(work)
         if rank != self.dst:
             return None
-        out = [parts[r][: shard_bounds(n_total, r, world)[1] - shard_bounds(n_total, r, world)[0]]
-               for r in range(world)]
-        return torch.cat(out, dim=0)
+        if n_total == world * q_max:                  # equal shards: the buffer is the batch
+            return out.view((n_total,) + tuple(t.shape[1:]))
+        self.wait()
+        sizes = [shard_bounds(n_total, r, world) for r in range(world)]
+        return torch.cat([out[r, : b1 - b0] for r, (b0, b1) in enumerate(sizes)], dim=0)
 
     def _shard_kwargs(self, kwargs, b0: int, b1: int, n_total: int) -> dict:
         kw = dict(kwargs)
-        kw["seed"] = self._shared_seed(kwargs)
+        kw["seed"] = self.last_seed = self._shared_seed(kwargs)
         for k in ("_noise", "_noise_fallback"):
             if k in kw:
                 kw[k] = slice_noise(kw[k], b0, b1, n_total)
