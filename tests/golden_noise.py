@@ -81,3 +81,24 @@ def gibbs_noise(case: dict, model, latent, dmax: int):
             out[it, 2 * j + 1, 0, :, 0, 0] = r["value"].float().view(-1).expand(B)
     assert pos == len(recs)
     return init, out
+
+
+def tie_mask(case: dict, model, b: int, s: int, width_tol: float, phase: int = 0):
+    """[b, s] particles whose recorded categorical choice (mdn component, softmax_nn class, KDE
+    point) had a CDF interval narrower than ``width_tol`` (make_golden_large.py records the
+    width): fp32 probabilities may legitimately pick a neighbour there.  None if the fixture
+    records no widths."""
+    per_node: Dict[str, list] = {}
+    for r in case["draws"]:
+        if r["phase"] != phase or r["node"] is None or r["kind"] != "cat" or "width" not in r:
+            continue
+        per_node.setdefault(r["node"], []).append(r["width"].float())
+    if not per_node:
+        return None
+    mask = torch.zeros(b, s, dtype=torch.bool)
+    for node, ws in per_node.items():
+        w = torch.cat(ws)
+        dc = model.out_dim(node) if model.cpds[node].kind == "softmax_nn" else 1
+        narrow = (w < width_tol).view(-1, s, dc).any(-1)          # [b | 1, s]
+        mask |= narrow.expand(b, s) if narrow.shape[0] == 1 else narrow
+    return mask

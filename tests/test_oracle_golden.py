@@ -106,3 +106,20 @@ def test_fixture_exercises_semantics():
                     seen.add("mcm_root_target_1xS")
     assert {("is_fallback", True), ("is_fallback", False), "is_nan_rows", "mcm_do_target",
             "mcm_root_target_1xS"} <= seen, seen
+
+
+def test_large_fixtures_span_every_kde_chunk():
+    """The large-M fixtures (make_golden_large.py) choose KDE points from all 16 inverse-CDF
+    chunks of the kernel (csrc kde_cb: 16-point blocks per chunk), at 4096 and 10,000 points,
+    and cover S = 2048 -- the sizes cfg4 / cfg5 run."""
+    from vectorizedbayesiannetwork_amd.plan import KDE_CHUNKS, _kde_cb
+    for name, m in (("large_kde4096", 4096), ("large_kde10000", 10000)):
+        fx = load_golden(name)
+        chunk = _kde_cb(m) * 16
+        hit = set()
+        for case in fx["cases"]:
+            for r in case["draws"]:
+                if r["kind"] == "cat" and r["node"] is not None and r["index"] is not None:
+                    hit |= set((r["index"] // chunk).tolist())
+        assert hit == set(range(KDE_CHUNKS)), (name, sorted(hit))
+    assert max(c["n_samples"] for c in load_golden("large_mix12")["cases"]) == 2048
