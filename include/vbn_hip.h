@@ -106,9 +106,11 @@ enum vbn_mode {
 
 /* One node of the topological walk (32 x int32, filled by the host plan packer).
  * reserved[0] = split-f16 W2 fragments; [1..4] = KDE point packs; [5] = wblk_off, [6] =
- * wblk_len: the NN CPD's weight block [W1 fragments | accumulator-init biases | split-f16 W2]
- * (params float offset, length in floats, a multiple of 256), which the walk stages into LDS
- * one step ahead (0 = the step runs no MLP); [7] = one-feature KDE point pack in the
+ * wblk_len: the NN CPD's weight block [W1 fragments | layer-1/2 accumulator-init biases |
+ * split-f16 W2 | W3 | b3], rounded up to a multiple of 256 floats (params float offset,
+ * length in floats), which the walk stages into LDS one step ahead (0 = the step runs no
+ * MLP); the exact-f32 W2 copy (off_w2) deliberately stays outside the block and is read from
+ * global memory on the rare exact path; [7] = one-feature KDE point pack in the
  * v_mfma_f32_32x32x2_f32 operand layout ([rows/32][2][32]: scaled point, |point|^2), or -1. */
 typedef struct vbn_step {
   int32_t kind, role, flags, act;
@@ -154,7 +156,10 @@ typedef struct vbn_walk_args {
   int32_t gibbs_thin;
   int32_t n_noise;         /* noise nodes per sweep (injected-noise stride, mode GIBBS) */
   int32_t wbuf_floats;     /* >= every step's wblk_len: size of each of the two LDS weight
-                              buffers shared by the waves of a workgroup                */
+                              buffers shared by the waves of a workgroup (the caller's
+                              contract; torch.ops.vbn_hip.* check it).  When the two buffers
+                              do not fit in LDS next to the value slots, the launch runs an
+                              unstaged kind set that reads the weights from params      */
   int32_t wave_particles;  /* particles per wave64: 64 (0 = 64) or 32, the half-wave form for
                               launches too small to fill the chip (Gibbs at a few thousand
                               chains): lanes 32-63 mirror lanes 0-31 (same particle and draws,

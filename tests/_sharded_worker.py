@@ -23,7 +23,10 @@ HOT_NODE_VALUE = 50.0        # off-manifold evidence in the last query (rank 1's
 def cases(vbn, target, ev):
     from vectorizedbayesiannetwork_amd.engines import ImportanceSampling, MonteCarloMarginalization, Query
     hot = {k: v.clone() for k, v in ev.items()}
-    k0 = sorted(hot)[0]
+    # an evidence node with latent parents: its log-weight varies across the particles, so an
+    # off-manifold value collapses that query's ESS (a root's would shift every weight alike)
+    par = vbn.model.parents
+    k0 = next(k for k in sorted(hot) if par[k] and not any(p in hot for p in par[k]))
     hot[k0][B - 1, 0] = HOT_NODE_VALUE
     q = Query(target, {k: v.cuda() for k, v in ev.items()})
     qh = Query(target, {k: v.cuda() for k, v in hot.items()})

@@ -329,19 +329,33 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   // 16 waves = 4 per SIMD at the kernel's register budget), larger workgroups on ties (one
   // weight copy per workgroup); the other kind sets run one wave per workgroup
   const int64_t per_wave = vbn_hip_lds_bytes(a->n_slots, a->max_out);
-  const bool stage = staged_kinds(km);
-  const int64_t wbuf_bytes = stage ? 2 * (int64_t)a->wbuf_floats * (int64_t)sizeof(float) : 0;
   // small launches (e.g. Gibbs: one wave per 8 chains) keep >= 2 workgroups per CU first
   const int64_t waves = (a->n_queries * (int64_t)a->n_samples + wp - 1) / wp;
   int nw = 0;
-  int64_t lds = 0, best = 0;
-  for (int w = stage ? WG_MAX_WAVES : 1; w >= 1; w >>= 1) {
-    const int64_t l = w * per_wave + wbuf_bytes;
-    if (l > 160 * 1024) continue;
-    if (w > 1 && waves / w < 2 * 256) continue;
-    const int64_t res = std::min<int64_t>(16, (160 * 1024 / l) * w);
-    if (res > best) { best = res; nw = w; lds = l; }
+  int64_t lds = 0;
+  auto shape = [&](bool stg) {
+    const int64_t wbuf_bytes = stg ? 2 * (int64_t)a->wbuf_floats * (int64_t)sizeof(float) : 0;
+    int64_t best = 0;
+    nw = 0;
+    for (int w = stg ? WG_MAX_WAVES : 1; w >= 1; w >>= 1) {
+      const int64_t l = w * per_wave + wbuf_bytes;
+      if (l > 160 * 1024) continue;
+      if (w > 1 && waves / w < 2 * 256) continue;
+      const int64_t res = std::min<int64_t>(16, (160 * 1024 / l) * w);
+      if (res > best) { best = res; nw = w; lds = l; }
+    }
+  };
+  bool stage = staged_kinds(km);
+  shape(stage);
+#ifndef VBN_KM_ONLY
+  if (stage && nw == 0) {
+    // the two LDS weight buffers do not fit next to the value slots (very wide MLP fan-in):
+    // run the smallest unstaged kind set covering the plan, which reads weights from the blob
+    km = (want & 32u) ? 63u : 23u;
+    stage = false;
+    shape(false);
   }
+#endif
   if (nw == 0) return fail(VBN_E_LDS, "vbn_hip_walk: plan needs more than 160 KiB of LDS per wave");
   if (a->mode == VBN_MODE_GIBBS &&
       (a->n_samples != 8 || a->gibbs_iters <= 0 || a->gibbs_burn_in < 0 || a->gibbs_burn_in >= a->gibbs_iters ||

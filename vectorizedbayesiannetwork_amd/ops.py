@@ -20,7 +20,7 @@ import torch
 from torch import Tensor
 
 from . import _lib
-from .plan import MODE_GIBBS, STEP_INTS
+from .plan import MODE_GIBBS, S_WBLK_LEN, STEP_INTS
 
 __all__ = ["walk", "walk_segment", "normalize_weights", "rb_epilogue", "resample", "posterior_stats"]
 
@@ -75,6 +75,18 @@ def _walk_segment_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries
     return params.new_empty(total if want_lp else 0), params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))
 
 
+def _check_wbuf(op: str, steps: Tensor, begin: int, end: int, wbuf: int) -> None:
+    """``wbuf`` (floats per LDS weight buffer) must hold every staged weight block of the
+    steps walked.  Step tables from the plan packer carry their maximum (``_vbn_wblk_max``);
+    any other table costs one device read here."""
+    need = getattr(steps, "_vbn_wblk_max", None)
+    if need is None:
+        need = int(steps[begin:end, S_WBLK_LEN].max().item()) if end > begin else 0
+    if wbuf < need:
+        raise ValueError(f"vbn_hip::{op}: wbuf={wbuf} floats is smaller than the largest weight block "
+                         f"of the step table ({need} floats)")
+
+
 def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                  fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
                  offset, want_lp, kind_mask, state, state_flags, step_begin, step_end, wbuf):
@@ -92,6 +104,7 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
     step_end = steps.shape[0] if step_end < 0 else step_end
     if not 0 <= step_begin <= step_end <= steps.shape[0]:
         raise ValueError(f"vbn_hip::walk: bad step range [{step_begin}, {step_end})")
+    _check_wbuf("walk", steps, step_begin, step_end, wbuf)
     total = n_queries * n_samples
     if state_flags:
         if state is None:
@@ -172,6 +185,7 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
         _check_dev(name, t, dt, device)
     if steps.dim() != 2 or steps.shape[1] != STEP_INTS:
         raise ValueError("vbn_hip::gibbs_walk: steps must be [n_steps, 32]")
+    _check_wbuf("gibbs_walk", steps, 0, steps.shape[0], wbuf)
     if iters <= 0 or not 0 <= burn_in < iters or thin <= 0 or out_dim <= 0:
         raise ValueError("vbn_hip::gibbs_walk: need iters > burn_in >= 0, thin > 0, out_dim > 0")
     total = n_queries * 8

@@ -171,8 +171,8 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     w2f = np.zeros((16, 64), np.float32)
     for s in range(16):
         w2f[s] = w2[lane & 31, _ROWS[lane >> 5, s]]
-    # weight block staged into LDS by the walk (one step ahead): W1 | biases | split-f16 W2,
-    # contiguous, 16-byte aligned pieces
+    # weight block staged into LDS by the walk (one step ahead): W1 | biases | split-f16 W2 |
+    # W3 | b3, contiguous, 16-byte aligned pieces (the exact-f32 W2 copy stays outside)
     offs["w1"] = blob.add(w1f)
     offs["wblk"] = offs["w1"]
     # accumulator init: [layer][group g][half h][register r] = b[row(r, h)] (one copy per group)
@@ -540,8 +540,10 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
     max_out = max([packed.nodes[n].n_out for n in order] + [1])
     if any(packed.nodes[n].kind == KIND_ID["kde"] for n in order):
         max_out = max(max_out, KDE_CHUNKS)
+    steps_t = torch.from_numpy(steps).to(dev) if len(order) else torch.zeros(1, STEP_INTS, dtype=torch.int32, device=dev)
+    steps_t._vbn_wblk_max = int(steps[:, S_WBLK_LEN].max()) if len(order) else 0   # ops._check_wbuf
     return QueryPlan(
-        steps=torch.from_numpy(steps).to(dev) if len(order) else torch.zeros(1, STEP_INTS, dtype=torch.int32, device=dev),
+        steps=steps_t,
         in_cols=t(in_cols), out_cols=t(out_cols), n_steps=len(order), n_slots=max(n_slots, 1),
         max_out=max_out, fixed_nodes=fixed_nodes, fixed_ld=max(c, 1), noise_nodes=noise_nodes,
         out_nodes=list(out_nodes), mode=mode, slot_of=slot_of, kind_mask=kind_mask,
@@ -635,6 +637,7 @@ def build_gibbs_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Seque
     tab[sel, S_WBLK_OFF] = 0                                              # no MLP on these rows
     tab[sel, S_WBLK_LEN] = 0
     steps = torch.from_numpy(tab).to(packed.device)
+    steps._vbn_wblk_max = int(tab[:, S_WBLK_LEN].max())                  # ops._check_wbuf
     return GibbsPlan(init=init, steps=steps, n_steps=len(table), latent=lat, target=target,
                      n_noise=max(2 * len(lat), 1), in_cols=full.in_cols, kind_mask=full.kind_mask,
                      wbuf=int(tab[:, S_WBLK_LEN].max()))
