@@ -67,9 +67,11 @@ enum vbn_role {
   VBN_ROLE_SKIP = 0,
   VBN_ROLE_LATENT = 1,
   VBN_ROLE_FIXED = 2,
-  VBN_ROLE_PARAMS = 3,  /* write the CPD's conditional parameters, no draw (RB target):
+  VBN_ROLE_PARAMS = 3,  /* write the CPD's conditional parameters, no draw (RB target,
+                           CPDHandle.conditional, vbn/core/cpd_handle.py:40-118):
                            gaussian_nn / linear_gaussian: loc[D] ++ scale[D];
-                           softmax_nn (D = 1): class probabilities[C]                   */
+                           softmax_nn: class probabilities[D][C];
+                           mdn: softmax(logits)[K] ++ loc[K][D] ++ scale[K][D]           */
   VBN_ROLE_SELECT = 4,  /* Gibbs: softmax over the 8 candidate lanes of a chain, choose one,
                            broadcast its value (out_col, out_dim) to the chain's lanes     */
   VBN_ROLE_COLLECT = 5  /* Gibbs: after burn-in, every thin-th sweep, write the target     */

@@ -23,7 +23,8 @@ import networkx as nx
 import torch
 
 from .engines import Query, infer_batch_size
-from .model import BNModel, load_checkpoint, model_from_checkpoint, model_from_vbn
+from .handle import CPDHandle
+from .model import BNModel, checkpoint_from_model, load_checkpoint, model_from_checkpoint, model_from_vbn
 from .registry import INFERENCE_REGISTRY, SAMPLING_REGISTRY
 
 __all__ = ["VBN", "ConfigItem", "defaults"]
@@ -176,6 +177,46 @@ class VBN:
 
     def to_device(self, device) -> None:
         self.device = torch.device(device)
+
+    # ---- persistence (reference vbn.py:644-734) ------------------------------------------
+    def save(self, path: str, *, include_configs: bool = True, extra: Optional[dict] = None) -> None:
+        """Write the reference checkpoint format: ``path`` ending in .pt/.pth/.ckpt is the
+        file; otherwise a directory gets ``checkpoint.pt`` + ``meta.json``.  The reference's
+        ``VBN.load`` reads it back (tests/test_model.py checks the round trip)."""
+        import json
+        import os
+        config = None
+        if include_configs:
+            for label, cfg in (("inference", self._inference_config), ("sampling", self._sampling_config)):
+                if cfg and cfg.get("callable"):
+                    raise ValueError(f"Cannot serialize callable {label} method: {cfg.get('name')}")
+            config = {"learning": None, "inference": self._inference_config,
+                      "sampling": self._sampling_config, "update": None}
+        ck = checkpoint_from_model(self.model, seed=self.seed, device=str(self.device), config=config, extra=extra)
+        _, ext = os.path.splitext(path)
+        meta_path = None
+        if ext in {".pt", ".pth", ".ckpt"}:
+            ck_path = path
+        else:
+            os.makedirs(path, exist_ok=True)
+            ck_path, meta_path = os.path.join(path, "checkpoint.pt"), os.path.join(path, "meta.json")
+        torch.save(ck, ck_path)
+        if meta_path is not None:
+            summary = {"meta": ck["meta"], "dag": ck["dag"],
+                       "nodes": {k: {"cpd_key": v["cpd_key"]} for k, v in ck["nodes"].items()},
+                       "config": ck.get("config")}
+            with open(meta_path, "w", encoding="utf-8") as f:
+                json.dump(summary, f, indent=2, default=str)
+
+    # ---- CPD access (reference vbn.py:634-641) -------------------------------------------
+    def cpd(self, node: str) -> CPDHandle:
+        return CPDHandle(self, node)
+
+    def get_cpd(self, node: str) -> CPDHandle:
+        return CPDHandle(self, node)
+
+    def get_cpds(self) -> Dict[str, CPDHandle]:
+        return {node: CPDHandle(self, node) for node in self.dag.nodes()}
 
     # ---- configuration ------------------------------------------------------------------
     def set_inference_method(self, method, **kwargs):

@@ -683,7 +683,8 @@ __device__ __forceinline__ int inv_cdf(int K, float u, F prob) {
 // ------------------------------------------------------------------------------------------
 // mdn (mdn.py:185-272)
 //   non-root: scr = [logits K][comp k: loc D, raw_scale D];  tail: min_scale
-//   root    : tail = pi[K], log_pi[K], loc[K*D], scale[K*D], log_scale[K*D], var[K*D]
+//   root    : tail = pi[K], log_pi[K], loc[K*D], scale[K*D], log_scale[K*D], var[K*D],
+//             softmax(logits)[K] (unclamped, for the PARAMS role)
 // ------------------------------------------------------------------------------------------
 template <unsigned KM>
 __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step& st, const Lane& L, float& lp) {
@@ -705,8 +706,32 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
     }
   };
   if (root) draws();
+  if (!root) run_mlp<KM>(A, st, L, draws);
+  if (st.role == VBN_ROLE_PARAMS) {
+    // mixture parameters (CPDHandle.conditional, cpd_handle.py:72-88): softmax(logits) [K]
+    // (no clamp), loc [K][D], scale [K][D]; root: the host's softmax / loc / scale constants
+    if (root) {
+      for (int k = 0; k < K; ++k) vwrite(L, st.out_col + k, t[2 * K + 4 * K * D + k]);
+      for (int j = 0; j < K * D; ++j) {
+        vwrite(L, st.out_col + K + j, t[2 * K + j]);
+        vwrite(L, st.out_col + K + K * D + j, t[2 * K + K * D + j]);
+      }
+      return;
+    }
+    const float ms = t[0];
+    float mx = -INFINITY, se = 0.f;
+    for (int k = 0; k < K; ++k) mx = fmaxf(mx, scr[k * WAVE + lane]);
+    for (int k = 0; k < K; ++k) se += __expf(scr[k * WAVE + lane] - mx);
+    for (int k = 0; k < K; ++k) vwrite(L, st.out_col + k, __expf(scr[k * WAVE + lane] - mx) / se);
+    for (int k = 0; k < K; ++k)
+      for (int d = 0; d < D; ++d) {
+        vwrite(L, st.out_col + K + k * D + d, scr[(K + k * 2 * D + d) * WAVE + lane]);
+        vwrite(L, st.out_col + K + K * D + k * D + d,
+               softplus_t(scr[(K + k * 2 * D + D + d) * WAVE + lane]) + ms);
+      }
+    return;
+  }
   if (!root) {
-    run_mlp<KM>(A, st, L, draws);
     min_scale = t[0];
     // pi = softmax(logits).clamp_min(1e-5); pi /= sum (mdn.py:227-228)
     lmax = -INFINITY;
@@ -806,9 +831,9 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
     for (int c = 0; c < C; ++c) m = fmaxf(m, logit(c));
     float se = 0.f;
     for (int c = 0; c < C; ++c) se += __expf(logit(c) - m);
-    if (st.role == VBN_ROLE_PARAMS) {                   // softmax(logits) (RB target, D = 1)
-      for (int c = 0; c < C; ++c) vwrite(L, st.out_col + c, __expf(logit(c) - m) / se);
-      return;
+    if (st.role == VBN_ROLE_PARAMS) {   // softmax(logits) per dim: [D][C] (RB target: D = 1)
+      for (int c = 0; c < C; ++c) vwrite(L, st.out_col + d * C + c, __expf(logit(c) - m) / se);
+      continue;
     }
     const bool disc = (st.aux1 >> d) & 1;
     const cfloat* e = edges + d * (C + 1);

@@ -30,6 +30,7 @@ __all__ = [
     "model_from_vbn",
     "record_from_cpd",
     "random_init_model",
+    "checkpoint_from_model",
     "KIND_DEFAULTS",
 ]
 
@@ -194,6 +195,50 @@ def model_from_checkpoint(ckpt: Mapping[str, Any] | str) -> BNModel:
     )
 
 
+CLASS_NAME = {v: k for k, v in _CLASS_TO_KIND.items()}
+
+
+def checkpoint_from_model(model: BNModel, *, seed: Optional[int] = None, device: str = "cpu",
+                          config: Optional[Dict[str, Any]] = None, extra: Optional[dict] = None,
+                          version: str = "0.3.0") -> Dict[str, Any]:
+    """The reference ``VBN.save`` checkpoint dict (reference vbn/vbn.py:644-734) of ``model``:
+    ``{dag, nodes, meta, extra[, config]}`` with per-node ``cpd_key, class_name, input_dim,
+    output_dim, seed, init_kwargs, state_dict, extra_state`` in topological order; every
+    ``state_dict`` carries the ``_extra_state`` entry BaseCPD adds (core/base.py:75-81), so the
+    reference's strict ``load_state_dict`` accepts it.  Tensors and builtins only."""
+    nodes_state: Dict[str, Dict[str, Any]] = {}
+    dtype = "torch.float32"
+    for node in model.topo:
+        rec = model.cpds[node]
+        extra_state = None
+        if rec.kind == "kde":
+            extra_state = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in (rec.extra or {}).items()}
+        sd = {k: v.clone() for k, v in rec.state.items()}
+        sd["_extra_state"] = extra_state
+        nodes_state[node] = {
+            "cpd_key": rec.kind,
+            "class_name": CLASS_NAME[rec.kind],
+            "input_dim": int(rec.input_dim),
+            "output_dim": int(rec.output_dim),
+            "seed": seed,
+            "init_kwargs": {k: (tuple(v) if isinstance(v, list) else v) for k, v in rec.hparams.items()},
+            "state_dict": sd,
+            "extra_state": extra_state,
+        }
+    ck: Dict[str, Any] = {
+        "dag": {"nodes": list(model.nodes), "edges": [tuple(e) for e in model.edges],
+                "topological_order": list(model.topo),
+                "parents": {n: list(model.parents.get(n, [])) for n in model.nodes}},
+        "nodes": nodes_state,
+        "meta": {"vbn_version": version, "torch_version": str(torch.__version__), "dtype": dtype,
+                 "device": str(device), "seed": seed},
+        "extra": extra,
+    }
+    if config is not None:
+        ck["config"] = config
+    return ck
+
+
 def record_from_cpd(cpd: Any, kind: Optional[str] = None) -> CPDRecord:
     """Read a live reference CPD module duck-typed (no reference import)."""
     if kind is None:
@@ -324,6 +369,7 @@ def random_init_model(g: nx.DiGraph, kinds: Mapping[str, str], data: Mapping[str
             state["std_x"] = _std(par) if par is not None else torch.ones(0)
             state["mean_y"] = x.mean(0)
             state["std_y"] = _std(x)
+            state["_stats_ready"] = torch.tensor(True)
             if d_in == 0:
                 state["_loc"] = torch.randn(d_out, generator=gen) * 0.1
                 state["_log_scale"] = torch.randn(d_out, generator=gen) * 0.1

@@ -254,7 +254,8 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
             log_scale = torch.log(scale)
             offs["tail"] = blob.add(np.concatenate([
                 _np(pi), _np(torch.log(pi)), _np(st["_loc"]).reshape(-1), _np(scale).reshape(-1),
-                _np(log_scale).reshape(-1), _np(torch.exp(2 * log_scale)).reshape(-1)]))
+                _np(log_scale).reshape(-1), _np(torch.exp(2 * log_scale)).reshape(-1),
+                _np(torch.softmax(st["_logits"], dim=-1))]))
         else:
             offs.update(_pack_mlp(blob, rec, standardize=False))
             n_out = offs.pop("n_out")
@@ -403,8 +404,9 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
     the MLPs' hidden layer on the exact f32 MFMA chain instead of the split-f16 product;
     ``kde_valu``: KDE pairwise distances on packed VALU instead of the 16x16x4 f32 MFMA tile.
     ``params``: nodes whose conditional parameters are written instead of a draw (role
-    PARAMS; gaussian_nn / linear_gaussian: loc ++ scale, softmax_nn with D = 1: class
-    probabilities) -- the Rao-Blackwellized target.
+    PARAMS; gaussian_nn / linear_gaussian: loc ++ scale, softmax_nn: class probabilities
+    [D][C], mdn: softmax(logits) [K] ++ loc [K][D] ++ scale [K][D]) -- the Rao-Blackwellized
+    target and CPDHandle.conditional.
     """
     model = packed.model
     latent_s, fixed_s, logp_s, skip_s = set(latent), set(fixed), set(logp), set(skip)
@@ -423,10 +425,12 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
             return model.out_dim(n)
         rec = model.cpds[n]
         if rec.kind in ("gaussian_nn", "linear_gaussian"):
-            return 2 * model.out_dim(n)
-        if rec.kind == "softmax_nn" and model.out_dim(n) == 1:
-            return int(rec.hp("n_classes"))
-        raise ValueError(f"no parameter output for {rec.kind} node {n} with {model.out_dim(n)} dims")
+            return 2 * model.out_dim(n)                               # loc ++ scale
+        if rec.kind == "softmax_nn":
+            return model.out_dim(n) * int(rec.hp("n_classes"))        # class probabilities [D][C]
+        if rec.kind == "mdn":
+            return int(rec.hp("n_components")) * (1 + 2 * model.out_dim(n))  # weights, loc, scale
+        raise ValueError(f"no parameter output for {rec.kind} node {n}")
     # liveness: last step index reading each node's columns
     pos = {n: i for i, n in enumerate(order)}
     last = {n: pos[n] for n in order}
