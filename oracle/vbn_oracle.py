@@ -513,6 +513,52 @@ def cpd_log_prob(rec: CPDRecord, x: torch.Tensor, parents: Optional[torch.Tensor
 
 
 # ----------------------------------------------------------------------------------------
+# per-node CPD surface (reference core/base.py:55-59, core/cpd_handle.py:40-118, 348-404)
+# ----------------------------------------------------------------------------------------
+
+def cpd_forward(rec: CPDRecord, parents: Optional[torch.Tensor], n: int, draws) -> Dict[str, torch.Tensor]:
+    """BaseCPD.forward: sample, log_prob of the sample, pdf = exp(log_prob)."""
+    s = cpd_sample(rec, parents, n, draws)
+    lp = cpd_log_prob(rec, s, parents)
+    return {"samples": s, "log_prob": lp, "pdf": torch.exp(lp)}
+
+
+def conditional(rec: CPDRecord, parents: Optional[torch.Tensor], n_samples: int, draws) -> Dict[str, object]:
+    """CPDHandle.conditional's parameter branches (cpd_handle.py:40-118) for the hot-path CPDs."""
+    st = rec.state
+    p3 = None if parents is None else (parents.unsqueeze(1) if parents.dim() == 2 else parents)
+    if rec.kind == "linear_gaussian":                                        # 41-55
+        scale = _lg_scale(rec)
+        if p3 is None:
+            return {"format": "normal_params", "mean": st["_bias"].view(1, 1, -1), "std": scale.view(1, 1, -1)}
+        loc = p3 @ st["_weight"] + st["_bias"]
+        return {"format": "normal_params", "mean": loc, "std": scale.view(1, 1, -1).expand_as(loc)}
+    if rec.kind == "gaussian_nn":                                            # 59-67 via _params
+        loc, scale = _gnn_root_loc_scale(rec) if p3 is None else _gnn_loc_scale(rec, p3)
+        return {"format": "normal_params", "mean": loc, "std": scale}
+    if rec.kind == "mdn":                                                    # 71-87
+        k, d = int(rec.hp("n_components")), rec.output_dim
+        if p3 is None:
+            logits = st["_logits"].view(1, 1, -1)
+            loc = st["_loc"].view(1, 1, k, d)
+            scale = _softplus_min(st["_log_scale"], rec.hp("min_scale")).view(1, 1, k, d)
+        else:
+            logits, loc, scale = _mdn_params(rec, p3)
+        return {"format": "mixture_params", "weights": torch.softmax(logits, dim=-1), "loc": loc, "scale": scale}
+    if rec.kind == "softmax_nn":                                             # 90-118
+        d, c = rec.output_dim, int(rec.hp("n_classes"))
+        if p3 is None:
+            logits = (st["_root_log_probs"] if bool(st["_root_ready"]) else st["_logits"]).view(1, 1, d, c)
+        else:
+            logits = _smx_logits(rec, p3)
+        return {"format": "categorical_probs", "probs": torch.softmax(logits, dim=-1), "k": c,
+                "support": st["_sample_values"]}
+    s = cpd_sample(rec, parents, n_samples, draws)                           # kde: 392-404
+    return {"format": "empirical_samples", "samples": s, "mean": s.mean(dim=1),
+            "std": s.std(dim=1, unbiased=False)}
+
+
+# ----------------------------------------------------------------------------------------
 # engines (reference inference/_core.py, monte_carlo_marginalization.py, importance_sampling.py,
 # likelihood_weighting.py, sampling/ancestral.py)
 # ----------------------------------------------------------------------------------------

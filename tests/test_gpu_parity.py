@@ -63,7 +63,7 @@ def _cases():
         has_kde = any(str(v["cpd_key"]) == "kde" for v in fx["model"]["nodes"].values())
         for i, case in enumerate(fx["cases"]):
             out.append(pytest.param(name, i, False, id=f"{name}-{i}-{case['engine']}"))
-            if has_kde and case["engine"] not in ("cpd", "posterior_stats"):
+            if has_kde and case["engine"] not in ("cpd", "posterior_stats", "conditional", "forward"):
                 # the alternative KDE distance path (packed VALU)
                 out.append(pytest.param(name, i, True, id=f"{name}-{i}-{case['engine']}-kde_valu"))
     return out
@@ -93,6 +93,27 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
         if "x" in case:
             lpx = C.cpd_log_prob(vbn, node, case["x"].cuda(), None if par is None else par.cuda())
             _close("cpd.log_prob(x)", lpx, O.cpd_log_prob(rec, case["x"], par), 2e-4, 1e-4)
+        return
+    if eng == "conditional":                  # CPDHandle.conditional (cpd_handle.py:348-404)
+        node = case["node"]
+        par = case["parents"]
+        got = vbn.cpd(node).conditional_tensors(None if par is None else par.cuda(), n_samples=n, _noise=nd0)
+        ref = O.conditional(model.cpds[node], par, n, O.ReplayDraws(case["draws"]))
+        assert got["format"] == ref["format"] == case["outputs"]["format"]
+        for k, v in ref.items():
+            if isinstance(v, torch.Tensor):
+                _close(f"conditional.{k}", got[k], v, S_ATOL, S_RTOL)
+            else:
+                assert got[k] == v, k
+        return
+    if eng == "forward":                      # BaseCPD.forward (core/base.py:55-59), one walk
+        node = case["node"]
+        par = case["parents"]
+        out = C.cpd_forward(vbn, node, None if par is None else par.cuda(), n, _noise=nd0)
+        ref = O.cpd_forward(model.cpds[node], par, n, O.ReplayDraws(case["draws"]))
+        _close("forward.samples", out.samples, ref["samples"], S_ATOL, S_RTOL)
+        _close("forward.log_prob", out.log_prob, ref["log_prob"], 2e-4, 1e-4)
+        _close("forward.pdf", out.pdf, ref["pdf"], P_ATOL, P_RTOL)
         return
     if eng == "posterior_stats":
         st = vbn._posterior_stats(case["pdf"].cuda(), case["samples_in"].cuda())

@@ -171,8 +171,8 @@ class CPDHandle:
         return t
 
     # ---- evaluation on the GPU ------------------------------------------------------------
-    def sample(self, parents, n_samples: int) -> torch.Tensor:
-        return C.cpd_sample(self._vbn, self._node, self._parents_tensor(parents), int(n_samples)).detach()
+    def sample(self, parents, n_samples: int, **kw) -> torch.Tensor:
+        return C.cpd_sample(self._vbn, self._node, self._parents_tensor(parents), int(n_samples), **kw).detach()
 
     def log_prob(self, x, parents) -> torch.Tensor:
         return C.cpd_log_prob(self._vbn, self._node, self._x_tensor(x), self._parents_tensor(parents)).detach()
@@ -180,8 +180,8 @@ class CPDHandle:
     def pdf(self, x, parents) -> torch.Tensor:
         return torch.exp(self.log_prob(x, parents))
 
-    def forward(self, parents, n_samples: int) -> C.CPDOutput:
-        out = C.cpd_forward(self._vbn, self._node, self._parents_tensor(parents), int(n_samples))
+    def forward(self, parents, n_samples: int, **kw) -> C.CPDOutput:
+        out = C.cpd_forward(self._vbn, self._node, self._parents_tensor(parents), int(n_samples), **kw)
         return C.CPDOutput(samples=out.samples.detach(), log_prob=out.log_prob.detach(), pdf=out.pdf.detach())
 
     def conditional_samples(self, parents, n_samples: int = 1024) -> torch.Tensor:
@@ -193,12 +193,13 @@ class CPDHandle:
     def conditional_pdf(self, x, parents) -> torch.Tensor:
         return self.pdf(x, parents)
 
-    def conditional_tensors(self, parents, *, n_samples: int = 1024) -> Dict[str, Any]:
-        """The fields of :meth:`conditional` as device tensors (no host copies)."""
+    def conditional_tensors(self, parents, *, n_samples: int = 1024, **kw) -> Dict[str, Any]:
+        """The fields of :meth:`conditional` as device tensors (no host copies); ``kw``
+        (``seed``, injected draws) goes to the kde sampler."""
         pt = self._parents_tensor(parents)
         kind, D = self._rec.kind, self.output_dim
         if kind == "kde":
-            s = self.sample(pt, n_samples)
+            s = self.sample(pt, n_samples, **kw)
             return {"format": "empirical_samples", "samples": s, "mean": s.mean(dim=1),
                     "std": s.std(dim=1, unbiased=False), "n_samples": int(n_samples)}
         prm = C.cpd_params(self._vbn, self._node, pt)                  # [B, 1 | S, W]
