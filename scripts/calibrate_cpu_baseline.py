@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Calibrate bench.py's CPU baseline (the oracle port) against the reference itself.
+
+Build container only (the reference never travels to the GPU box).  For each workload, two
+fresh child processes with the tuned glibc allocator and the same thread
+count time ``infer_posterior`` on the same synthetic model and queries:
+
+* ``ref``:  the reference's own ``VBN.load`` of our checkpoint (``VBN.save``, reference
+  format) and its ``infer_posterior`` under ``torch.no_grad()``;
+* ``port``: the oracle's restatement with the reference's torch RNG calls (bench.py
+  ``cpu_baseline_child``).
+
+One warm-up, median of 5 (1 for slow configs); prints port/ref time ratios (BASELINE.md
+requires 0.8-1.25).  Usage: python scripts/calibrate_cpu_baseline.py [cfg2 cfg3 anchor64]
+"""
+from __future__ import annotations
+
+import json
+import os
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.environ.get("VBN_REFERENCE", "/root/reference")
+QUERIES = {"cfg2": 1024, "anchor64": 1024, "cfg3": 64}
+
+
+def child(impl: str, cfg_name: str, n_queries: int, reps: int) -> None:
+    sys.path.insert(0, REPO)
+    import torch
+    import bench
+    from oracle import vbn_oracle as O
+    torch.set_num_threads(bench.cpu_threads())
+    cfg, model, target, ev_nodes = bench.build_model(cfg_name)
+    torch.manual_seed(2)
+    joint = O.ancestral(model, None, {}, {}, n_queries, O.TorchDraws())
+    ev = {n: joint[n][0].contiguous() for n in ev_nodes}
+    S, eng = cfg["S"], cfg["engine"]
+    if impl == "ref":
+        sys.path.insert(0, REF)
+        os.environ.setdefault("CI", "1")
+        import vbn as R
+        from vectorizedbayesiannetwork_amd import VBN
+        with tempfile.TemporaryDirectory() as d:
+            p = os.path.join(d, "m.pt")
+            VBN.from_model(model, device="cpu", seed=0).save(p)
+            rv = R.VBN.load(p, map_location="cpu")
+        rv.set_inference_method(eng, n_samples=S)
+
+        def one():
+            with torch.no_grad():
+                rv.infer_posterior({"target": target, "evidence": ev})
+    else:
+        def one():
+            with torch.no_grad():
+                if eng == "monte_carlo_marginalization":
+                    O.monte_carlo_marginalization(model, target, ev, {}, S, O.TorchDraws())
+                else:
+                    O.importance_sampling(model, target, ev, {}, S, O.TorchDraws())
+    one()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        one()
+        ts.append(time.perf_counter() - t0)
+    print(json.dumps({"impl": impl, "config": cfg_name, "queries": n_queries, "median_s": statistics.median(ts),
+                      "threads": torch.get_num_threads(), "times": ts}), flush=True)
+
+
+def main(argv):
+    if len(argv) > 1 and argv[1] == "--child":
+        child(argv[2], argv[3], int(argv[4]), int(argv[5]))
+        return 0
+    if not os.path.isdir(os.path.join(REF, "vbn")):
+        print(f"reference not found at {REF}; nothing to calibrate")
+        return 0
+    sys.path.insert(0, REPO)
+    import bench
+    env = dict(os.environ, **bench.CPU_ENV)
+    out = {}
+    for cfg_name in argv[1:] or ["cfg2", "cfg3", "anchor64"]:
+        nq = QUERIES[cfg_name]
+        res = {}
+        for impl in ("ref", "port"):
+            r = subprocess.run([sys.executable, __file__, "--child", impl, cfg_name, str(nq), "5"], env=env,
+                               capture_output=True, text=True, timeout=3600)
+            if r.returncode != 0:
+                raise RuntimeError(r.stderr[-3000:])
+            res[impl] = json.loads(r.stdout.strip().splitlines()[-1])
+        ratio = res["port"]["median_s"] / res["ref"]["median_s"]
+        out[cfg_name] = {"queries": nq, "ref_qps": nq / res["ref"]["median_s"], "port_qps": nq / res["port"]["median_s"],
+                         "port_over_ref_time": ratio, "threads": res["ref"]["threads"]}
+        print(json.dumps({cfg_name: out[cfg_name]}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv))
