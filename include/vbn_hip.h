@@ -90,6 +90,9 @@ enum vbn_role {
 #define VBN_F_BM_FIRST 512  /* lean walks: this step's Box-Muller pair also yields the next     */
                             /* VBN_F_BM_SECOND step's dim-0 normal (r sin; this step takes r cos) */
 #define VBN_F_BM_SECOND 1024
+#define VBN_F_MLP_GENERIC 2048  /* NN CPD with hidden_dims other than (32, 32): every layer as
+                                   exact f32 MFMA tiles through LDS; off_w2 points at the layer
+                                   table [L, (in, out, off_w, off_b) x L] (int32 in the blob)   */
 
 /* activations of the NN CPDs (reference gaussian_nn.py:19-24) */
 enum vbn_act { VBN_ACT_RELU = 0, VBN_ACT_TANH = 1, VBN_ACT_GELU = 2, VBN_ACT_ELU = 3 };
@@ -144,7 +147,8 @@ typedef struct vbn_walk_args {
   int32_t dmax;
   int32_t n_out_cols;
   int32_t mode;            /* enum vbn_mode                                        */
-  int32_t kind_mask;       /* CPD kinds walked: 1<<kind, | 32 if a non-relu activation */
+  int32_t kind_mask;       /* CPD kinds walked: 1<<kind, | 32 if a non-relu activation,
+                              | 512 if some NN CPD has hidden_dims other than (32, 32) */
   int64_t q_base;          /* global index of query 0 (multi-GPU shards)            */
   uint64_t seed;
   uint64_t offset;         /* RNG stream offset (one per engine call)               */

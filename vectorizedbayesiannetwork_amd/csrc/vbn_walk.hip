@@ -322,6 +322,8 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   for (unsigned m : masks) {
     if ((m & want) == want && __builtin_popcount(m) < __builtin_popcount(km)) km = m;
   }
+  const bool generic = ((unsigned)a->kind_mask & 512u) != 0;   // some MLP with other hidden_dims
+  if (generic) km = 63u;
 #ifdef VBN_KM_ONLY
   km = VBN_KM_ONLY;
 #endif
@@ -351,7 +353,7 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   if (stage && nw == 0) {
     // the two LDS weight buffers do not fit next to the value slots (very wide MLP fan-in):
     // run the smallest unstaged kind set covering the plan, which reads weights from the blob
-    km = (want & 32u) ? 63u : 23u;
+    km = ((want & 32u) || generic) ? 63u : 23u;
     stage = false;
     shape(false);
   }
@@ -369,7 +371,8 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   // kind set | 64: the half-wave (mirror) instantiation; | 128: the lean one
   const bool lean = !a->noise && !a->state && a->mode != VBN_MODE_GIBBS;
   const unsigned kmi = km | (wp == 32 ? 64u : 0u) | (lean && wp != 32 ? 128u : 0u) |
-                       (wp == 32 && !a->noise ? 256u : 0u);   // | 256: half-wave without injected draws
+                       (wp == 32 && !a->noise ? 256u : 0u) |  // | 256: half-wave without injected draws
+                       (generic ? 512u : 0u);                 // | 512: with the generic-MLP path
   hipError_t e = hipErrorInvalidDeviceFunction;
 #ifdef VBN_KM_ONLY
   // experiment builds (make exp KM=...): one instantiation only

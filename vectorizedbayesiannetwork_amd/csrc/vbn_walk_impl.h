@@ -529,10 +529,98 @@ __device__ __forceinline__ void mlp_nin(const vbn_walk_args& A, const vbn_step& 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Generic MLP (any hidden_dims, reference gaussian_nn.py:16-34 _build_mlp; VBN_F_MLP_GENERIC):
+// every layer -- input layer, hidden layers, head -- as exact f32 v_mfma_f32_32x32x2_f32 tiles
+// of 32 units x 32 particles, K in steps of 2, activations ping-ponged through the wave's LDS
+// scratch rows (layer input row k of particle n at buf[k][n]; conflict-free: lane halves read
+// rows 2t and 2t + 1).  Out of line so the (32, 32) hot path keeps its registers.
+//   off_w2 (step) -> layer table int32 [1 + 4 L]: L, then per layer (in, out, off_w, off_b);
+//   off_w : [ceil(out/32)][ceil(in/2)][64]  lane l: W[32 blk + (l & 31)][2 t + (l >> 5)] (0-padded)
+//   off_b : [ceil(out/32)][2][16]           b[32 blk + row(r, h)] (accumulator init, 0-padded)
+// Scratch rows: [0, n_out) the head's outputs (what the CPD epilogues read), then two buffers
+// of max(hidden) rows (plan.py sizes max_out = n_out + 2 max(hidden)).
+// ------------------------------------------------------------------------------------------
+template <int ACT, bool STD>
+__device__ __attribute__((noinline)) void mlp_generic(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  const int lane = L.lane, h = lane >> 5, col = lane & 31;
+  const cint* tab = CI(L.P + st.off_w2);
+  const int nl = tab[0];
+  int hmax = 1;
+  for (int li = 0; li + 1 < nl; ++li) hmax = max(hmax, tab[2 + 4 * li]);
+  float* buf0 = L.scr + st.n_out * WAVE;
+  float* buf1 = buf0 + hmax * WAVE;
+  bool nan_in = false;                            // torch keeps NaN through Linear / activation
+  for (int d = 0; d < st.n_in; ++d) {
+    const float v = L.vals[L.ic[st.in_off + d] * WAVE + lane];
+    nan_in |= (v != v);
+  }
+  for (int li = 0; li < nl; ++li) {
+    const int in = tab[1 + 4 * li], out = tab[2 + 4 * li];
+    const float* __restrict__ W = L.P + tab[3 + 4 * li];
+    const float* __restrict__ Bs = L.P + tab[4 + 4 * li];
+    const bool last = li + 1 == nl;
+    const float* src = (li & 1) ? buf0 : buf1;    // layer li >= 1 reads what li - 1 wrote
+    float* dst = last ? L.scr : ((li & 1) ? buf1 : buf0);
+    const int nblk = (out + 31) >> 5, t1 = (in + 1) >> 1;
+    for (int blk = 0; blk < nblk; ++blk) {
+      for (int g = 0; g < 2; ++g) {
+        f32x16 a = load_acc16(Bs + blk * 32 + 16 * h);
+        for (int t = 0; t < t1; ++t) {
+          const float w = W[(blk * t1 + t) * WAVE + lane];
+          float x;
+          if (li == 0) {
+            x = l1_operand<STD, 0>(A, st, L, t, g);
+          } else {
+            const int k = 2 * t + h;
+            x = k < in ? src[k * WAVE + col + 32 * g] : 0.f;
+          }
+          a = __builtin_amdgcn_mfma_f32_32x32x2f32(w, x, a, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = 32 * blk + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (row < out) dst[row * WAVE + col + 32 * g] = last ? a[r] : act_fn<ACT>(a[r]);
+        }
+      }
+    }
+    wave_sync();
+  }
+  if (nan_in)
+    for (int j = 0; j < st.n_out; ++j) L.scr[j * WAVE + lane] = __int_as_float(0x7fc00000);
+  wave_sync();
+}
+
+template <unsigned KM>
+__device__ __forceinline__ void run_mlp_generic(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  const bool sd = (st.flags & VBN_F_STANDARDIZE) != 0;
+  if (!(KM & 32) || st.act == VBN_ACT_RELU) {
+    if (sd) mlp_generic<VBN_ACT_RELU, true>(A, st, L); else mlp_generic<VBN_ACT_RELU, false>(A, st, L);
+    return;
+  }
+  if constexpr ((KM & 32) != 0) {
+    switch (st.act * 2 + (sd ? 1 : 0)) {
+      case 2: mlp_generic<VBN_ACT_TANH, false>(A, st, L); break;
+      case 3: mlp_generic<VBN_ACT_TANH, true>(A, st, L); break;
+      case 4: mlp_generic<VBN_ACT_GELU, false>(A, st, L); break;
+      case 5: mlp_generic<VBN_ACT_GELU, true>(A, st, L); break;
+      case 6: mlp_generic<VBN_ACT_ELU, false>(A, st, L); break;
+      default: mlp_generic<VBN_ACT_ELU, true>(A, st, L); break;
+    }
+  }
+}
+
 // KM bit 5: some NN CPD uses a non-relu activation; bit 6: half-wave instantiation.  ``pre``: the step's draws (see mlp_forward).
 template <unsigned KM, typename F>
 __device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
   constexpr bool MIR = (KM & 64) != 0;             // half-wave instantiation
+  if constexpr ((KM & 512) != 0) {                 // kind-set bit 9: plans with generic MLPs
+    if (st.flags & VBN_F_MLP_GENERIC) {            // hidden_dims other than (32, 32)
+      pre();
+      run_mlp_generic<KM>(A, st, L);
+      return;
+    }
+  }
   const bool sd = (st.flags & VBN_F_STANDARDIZE) != 0;
   if (!(KM & 32) || st.act == VBN_ACT_RELU) {
     if (sd) mlp_nin<VBN_ACT_RELU, true, MIR>(A, st, L, pre); else mlp_nin<VBN_ACT_RELU, false, MIR>(A, st, L, pre);
@@ -1744,12 +1832,15 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
 // half-wave (mirror) launch (include/vbn_hip.h wave_particles = 32), bit 7 the lean walk (no
 // injected draws, no segment state, not Gibbs: the production MCM / IS / LW / ancestral path;
 // measured cfg2 1.215 -> 1.19 ms, SGPR spills 35 -> 0), bit 8 no injected draws (with bit 6: the
-// production half-wave Gibbs sweeps; SGPR spills 34 -> 9).  Each is compiled in its
+// production half-wave Gibbs sweeps; SGPR spills 34 -> 9), bit 9 the generic-MLP path (plans
+// with hidden_dims other than (32, 32): only with the all-kinds set 63, so the out-of-line
+// mlp_generic call never touches the hot instantiations' registers).  Each is compiled in its
 // own object from walk_inst.hip (Makefile KIND_SETS must list the same values).
 #define VBN_WALK_KIND_SETS(X) \
   X(1) X(2) X(3) X(4) X(8) X(16) X(20) X(23) X(31) X(63) \
   X(65) X(66) X(67) X(68) X(72) X(80) X(84) X(87) X(95) X(127) \
   X(129) X(130) X(131) X(132) X(136) X(144) X(148) X(151) X(159) X(191) \
-  X(321) X(322) X(323) X(324) X(328) X(336) X(340) X(343) X(351) X(383)
+  X(321) X(322) X(323) X(324) X(328) X(336) X(340) X(343) X(351) X(383) \
+  X(575) X(639) X(703) X(895)
 #define VBN_LAUNCHER_(K) vbn_launch_walk_km##K
 #define VBN_LAUNCHER(K) VBN_LAUNCHER_(K)

@@ -30,7 +30,7 @@ from .model import BNModel, CPDRecord
 KIND_ID = {"gaussian_nn": 0, "linear_gaussian": 1, "mdn": 2, "kde": 3, "softmax_nn": 4}
 ROLE_SKIP, ROLE_LATENT, ROLE_FIXED, ROLE_PARAMS, ROLE_SELECT, ROLE_COLLECT = 0, 1, 2, 3, 4, 5
 F_LOGP, F_ROOT, F_SHARED, F_STANDARDIZE, F_CLIP, F_F32L2, F_KDE_VALU = 1, 2, 4, 8, 16, 32, 64
-F_KEEP, F_LPRESET, F_BM_FIRST, F_BM_SECOND = 128, 256, 512, 1024
+F_KEEP, F_LPRESET, F_BM_FIRST, F_BM_SECOND, F_MLP_GENERIC = 128, 256, 512, 1024, 2048
 ACT_ID = {"relu": 0, "tanh": 1, "gelu": 2, "elu": 3}
 WITHIN_ID = {"uniform": 0, "triangular": 1, "gaussian": 2}
 MODE_MCM, MODE_WEIGHTED, MODE_SAMPLE, MODE_GIBBS = 0, 1, 2, 3
@@ -43,7 +43,6 @@ WBLK_CHUNK = 256          # floats per LDS-DMA wave instruction (64 lanes x 16 B
 KDE_CHUNKS = 16
 KDE_REC_TAIL = 8       # weight-0 record rows after the last point (csrc kde_scan prefetch)
 MLP_HIDDEN = (32, 32)
-KDE_MAX_DIMS = 4
 MAX_NODES = 1 << 14
 MAX_NODE_DIMS = 1 << 8
 
@@ -147,22 +146,46 @@ def _np(t: torch.Tensor) -> np.ndarray:
     return t.detach().to("cpu", torch.float32).numpy()
 
 
+def _pack_mlp_generic(blob: _Blob, layers, offs: Dict[str, int]) -> Dict[str, int]:
+    """Layer table + fragments of csrc mlp_generic (hidden_dims other than (32, 32)): per
+    layer W fragments [ceil(out/32)][ceil(in/2)][64] and accumulator-init biases
+    [ceil(out/32)][2][16]; the table [L, (in, out, off_w, off_b) x L] is int32 in the blob."""
+    lane = np.arange(64)
+    table = [len(layers)]
+    for w, b in layers:
+        w, b = _np(w), _np(b)
+        out, nin = w.shape
+        nblk, t1 = -(-out // 32), -(-nin // 2)
+        wz = np.zeros((nblk * 32, 2 * t1), np.float32)
+        wz[:out, :nin] = w
+        frag = np.stack([np.stack([wz[32 * k + (lane & 31), 2 * t + (lane >> 5)] for t in range(t1)])
+                         for k in range(nblk)])                                   # [nblk, t1, 64]
+        bz = np.zeros(nblk * 32, np.float32)
+        bz[:out] = b
+        bias = np.stack([bz[32 * k + _ROWS] for k in range(nblk)])                # [nblk, 2, 16]
+        table += [nin, out, blob.add(frag), blob.add(bias)]
+    offs["w2"] = blob.add(np.asarray(table, np.int32).view(np.float32))
+    offs["n_out"] = int(_np(layers[-1][0]).shape[0])
+    offs["generic"] = 1
+    offs["scratch"] = offs["n_out"] + 2 * max([int(w.shape[0]) for w, _ in layers[:-1]] + [1])
+    return offs
+
+
 def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
-    """MFMA fragment layouts of csrc/vbn_walk_impl.h mlp_forward (biases as accumulator init)."""
+    """MFMA fragment layouts of csrc/vbn_walk_impl.h mlp_forward (biases as accumulator init);
+    other hidden_dims than (32, 32) get the generic layer-by-layer pack (mlp_generic)."""
     layers = rec.mlp_layers()
     hidden = tuple(int(w.shape[0]) for w, _ in layers[:-1])
-    if hidden != MLP_HIDDEN:
-        raise NotImplementedError(
-            f"{rec.kind}: hidden_dims={hidden}; the gfx950 MFMA path implements {MLP_HIDDEN} "
-            "(the reference default, vbn/configs/cpds/*.yaml)")
-    (w1, b1), (w2, b2), (w3, b3) = [(_np(w), _np(b)) for w, b in layers]
-    nin = w1.shape[1]
     offs: Dict[str, int] = {}
     if standardize:
         inv = (np.float32(1.0) / _np(rec.state["std_x"]).astype(np.float32)).astype(np.float32)
         offs["std"] = blob.add(np.concatenate([_np(rec.state["mean_x"]), inv]))
     else:
         offs["std"] = 0
+    if hidden != MLP_HIDDEN:
+        return _pack_mlp_generic(blob, layers, offs)
+    (w1, b1), (w2, b2), (w3, b3) = [(_np(w), _np(b)) for w, b in layers]
+    nin = w1.shape[1]
     t1 = (nin + 1) // 2
     w1z = np.zeros((32, 2 * t1), np.float32)
     w1z[:, :nin] = w1
@@ -179,15 +202,17 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     offs["b2"] = blob.add(np.stack([np.stack([b[_ROWS]] * 2) for b in (b1, b2)]))  # [2, 2, 2, 16]
     # split-f16 fragments of v_mfma_f32_32x32x16_f16: k-step s, lane l, element j ->
     # W2[l&31][16s + 8(j>>2) + 4(l>>5) + (j&3)]; hi = f16(w), lo = f16(w - hi)
-    if np.abs(w2).max() > 32768.0:
-        raise NotImplementedError(f"{rec.kind}: |W2| exceeds the f16 split range")
+    # weights beyond the f16 split range: the node always takes the exact f32 layer-2 chain
+    # (the split fragments are still packed, so the weight block layout does not change)
+    offs["f32l2"] = int(np.abs(w2).max() > 32768.0)
     j = np.arange(8)
     frag = np.zeros((2, 64, 8), np.float32)
     for s in range(2):
         for ln in range(64):
             frag[s, ln] = w2[ln & 31, 16 * s + 8 * (j >> 2) + 4 * (ln >> 5) + (j & 3)]
-    hi = frag.astype(np.float16)
-    lo = (frag - hi.astype(np.float32)).astype(np.float16)
+    with np.errstate(over="ignore", invalid="ignore"):
+        hi = frag.astype(np.float16)
+        lo = (frag - hi.astype(np.float32)).astype(np.float16)
     halfs = np.concatenate([hi, lo]).reshape(-1)                               # [4, 64, 8] f16
     offs["w2h"] = blob.add(halfs.view(np.float32))
     # head: row j = W3[j][row(r, 0)] (r < 16) ++ W3[j][row(r, 1)] (lane half h reads 16 at 16 h)
@@ -212,6 +237,7 @@ class NodePack:
     aux0: int
     aux1: int
     offs: Dict[str, int]
+    scratch: int = 0    # LDS scratch rows the node's MLP needs (head outputs + generic buffers)
 
 
 def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
@@ -267,8 +293,6 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
         pts_y = rec.extra["targets"].float()
         m = int(pts_y.shape[0])
         dp = int(pts_p.shape[1]) if pts_p.dim() == 2 else 0
-        if dp > KDE_MAX_DIMS or D > KDE_MAX_DIMS:
-            raise NotImplementedError(f"kde with {dp} parent / {D} target dims (max {KDE_MAX_DIMS})")
         if m == 0:
             raise RuntimeError("KDECPD is not fitted yet.")
         bw = float(rec.hp("bandwidth"))
@@ -329,8 +353,13 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
             n_out = offs.pop("n_out")
     else:
         raise ValueError(kind)
+    if offs.pop("generic", 0):
+        flags |= F_MLP_GENERIC
+    if offs.pop("f32l2", 0):
+        flags |= F_F32L2
+    scratch = offs.pop("scratch", n_out)
     return NodePack(kind=KIND_ID[kind], flags=flags, act=max(act, 0), n_in=rec.input_dim,
-                    out_dim=D, k=k, n_out=n_out, aux0=aux0, aux1=aux1, offs=offs)
+                    out_dim=D, k=k, n_out=n_out, aux0=aux0, aux1=aux1, offs=offs, scratch=scratch)
 
 
 class PackedModel:
@@ -356,7 +385,7 @@ class PackedModel:
         host = torch.from_numpy(blob.finish())
         self.params = host.to(self.device)
         self.node_id = {n: i for i, n in enumerate(model.topo)}
-        self.max_out = max([p.n_out for p in self.nodes.values()] + [1])
+        self.max_out = max([p.scratch for p in self.nodes.values()] + [1])
         self.has_kde = any(p.kind == KIND_ID["kde"] for p in self.nodes.values())
         self.dmax = max(model.out_dim(n) for n in model.topo)
 
@@ -375,7 +404,8 @@ class QueryPlan:
     out_nodes: List[str]
     mode: int
     slot_of: Dict[str, int]
-    kind_mask: int = 63       # CPD kinds the walk evaluates (selects the kernel instantiation)
+    kind_mask: int = 63       # CPD kinds the walk evaluates (selects the kernel instantiation;
+                              # | 32 non-relu activations, | 512 generic-MLP nodes)
     wbuf: int = 0             # floats per LDS weight buffer (max wblk_len over the steps)
 
 
@@ -541,7 +571,9 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
             kind_mask |= 1 << npk.kind
             if npk.n_out and npk.act != ACT_ID["relu"]:
                 kind_mask |= 32
-    max_out = max([packed.nodes[n].n_out for n in order] + [1])
+            if npk.flags & F_MLP_GENERIC:
+                kind_mask |= 512                 # csrc kind-set bit 9: the generic-MLP path
+    max_out = max([packed.nodes[n].scratch for n in order] + [1])
     if any(packed.nodes[n].kind == KIND_ID["kde"] for n in order):
         max_out = max(max_out, KDE_CHUNKS)
     steps_t = torch.from_numpy(steps).to(dev) if len(order) else torch.zeros(1, STEP_INTS, dtype=torch.int32, device=dev)
