@@ -59,7 +59,7 @@ def main():
     ap.add_argument("--wave-particles", type=int, default=None, help="32 / 64 (default: the engine's choice)")
     args = ap.parse_args()
     torch.cuda.set_device(0)
-    cfg, g, model, vbn, query = Bm.build_workload("cfg2", "cuda:0", 0)
+    cfg, model, vbn, query = Bm.build_workload("cfg2", "cuda:0", 1)
     B = args.chains
     reps_ev = -(-B // cfg["B"])                      # more chains than cfg2 queries: tile the evidence rows
     query = {"target": query["target"],

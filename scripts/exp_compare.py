@@ -26,7 +26,7 @@ def child(cfg_name: str, out_path: str, engine_kw: str):
     from vectorizedbayesiannetwork_amd import engines as E
 
     torch.cuda.set_device(0)
-    cfg, g, model, vbn, query = build_workload(cfg_name, "cuda:0", 0)
+    cfg, model, vbn, query = build_workload(cfg_name, "cuda:0", 1)
     B, S = cfg["B"], cfg["S"]
     kw = json.loads(engine_kw)
     vbn.set_inference_method(cfg["engine"], n_samples=S, **kw)

@@ -462,12 +462,28 @@ __device__ __forceinline__ bool mlp_l1_act(const vbn_walk_args& A, const vbn_ste
   return __any(big > 0x47000000);
 }
 
-// One NN node for the wave's 64 particles from the LDS-staged weight block: group 0 (layer 1,
-// range check, layer 2 split-f16 on MFMA), then group 1, the head on both.  ``pre`` (the
-// step's draws, independent of the MLP) runs after group 0's fragment reads are issued.  An
-// f16-range miss in either group, or VBN_F_F32L2, sends both groups to the exact f32 chain
-// (layer 1 recomputed there from the blob).
-template <int ACT, bool STD, int NIN, bool MIR, typename F>
+// Head outputs with a compile-time count (NOUT > 0): straight-line code, so the scheduler can
+// place it beside the other group's layer-2 MFMAs (same operations as head_outputs).
+template <int NOUT>
+__device__ __forceinline__ void head_outputs_n(const float* __restrict__ w3, const float* __restrict__ b3,
+                                               float* __restrict__ scr, const float (&y0)[16],
+                                               const float (&y1)[16], bool nan_in) {
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    const float4* wa = reinterpret_cast<const float4*>(w3 + 32 * j);
+    const float4 va[4] = {wa[0], wa[1], wa[2], wa[3]};
+    scr[j * WAVE] = head_dot(va, y0, y1, b3[j], nan_in);
+  }
+}
+
+// One NN node for the wave's 64 particles from the LDS-staged weight block.  Group 0 (layer 1,
+// layer 2 split-f16 on MFMA), group 1, the head on both -- one basic block: the f16 range
+// check only ORs a wave-uniform flag, and the rare exact path (an activation beyond the split
+// range, or VBN_F_F32L2) re-runs the node on the exact f32 chain after the head and overwrites
+// its outputs.  Without branches between them, the compiler can issue group 1's layer-1 /
+// split VALU work and group 0's head in the shadow of the other group's MFMAs.  ``pre`` (the
+// step's draws) runs after group 0's fragment reads are issued.
+template <int ACT, bool STD, int NIN, bool MIR, int NOUT, typename F>
 __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
   const int lane = L.lane;
   const int nin = NIN > 0 ? NIN : st.n_in;
@@ -480,31 +496,34 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
     nan_in |= (v != v);
   }
   f32x16 h0, h1;
-  bool exact = (st.flags & VBN_F_F32L2) != 0;
-  bool pre_done = false;
-  if (!exact) {
+  bool big;
+  {
     float y[16];
-    pre_done = true;
-    if (mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 0, y, pre)) {
-      exact = true;
-    } else {
-      const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
-      h0 = layer2_split(wq, load_acc16(b2), y);
-    }
-  }
-  if (!exact) {
-    float y[16];
+    big = mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 0, y, pre);
+    const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
+    h0 = layer2_split(wq, load_acc16(b2), y);
     if constexpr (MIR) {
       h1 = h0;                                    // group 1 = group 0's particles
-    } else if (mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 1, y, [] {})) {
-      exact = true;
     } else {
-      const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
-      h1 = layer2_split(wq, load_acc16(b2 + 32), y);
+      float y1[16];
+      big |= mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 1, y1, [] {});
+      h1 = layer2_split(wq, load_acc16(b2 + 32), y1);
     }
   }
-  if (exact) {
-    if (!pre_done) pre();
+  if constexpr (NOUT > 0) {
+    float y0[16], y1[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      y0[r] = act_fn<ACT>(h0[r]);
+      y1[r] = act_fn<ACT>(h1[r]);
+    }
+    head_outputs_n<NOUT>(W + (st.off_w3 - WBLK_OFF(st)) + 16 * (lane >> 5), W + (st.off_b3 - WBLK_OFF(st)),
+                         L.scr + lane, y0, y1, nan_in);
+    wave_sync();
+  } else {
+    mlp_head<ACT>(st, L, W, h0, h1, nan_in);
+  }
+  if (big || (st.flags & VBN_F_F32L2)) {          // rare: the exact f32 chain, outputs overwritten
     const float* __restrict__ Wg = L.P + WBLK_OFF(st);
     float y[16];
     mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 0, y, [] {});
@@ -515,17 +534,17 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
       mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 1, y, [] {});
       h1 = layer2_exact(st, L, 1, y);
     }
+    mlp_head<ACT>(st, L, W, h0, h1, nan_in);
   }
-  mlp_head<ACT>(st, L, W, h0, h1, nan_in);
 }
 
-template <int ACT, bool STD, bool MIR, typename F>
+template <int ACT, bool STD, bool MIR, int NOUT, typename F>
 __device__ __forceinline__ void mlp_nin(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
   switch (st.n_in) {
-    case 1: mlp_forward<ACT, STD, 1, MIR>(A, st, L, pre); break;
-    case 2: mlp_forward<ACT, STD, 2, MIR>(A, st, L, pre); break;
-    case 3: mlp_forward<ACT, STD, 3, MIR>(A, st, L, pre); break;
-    default: mlp_forward<ACT, STD, 0, MIR>(A, st, L, pre); break;
+    case 1: mlp_forward<ACT, STD, 1, MIR, NOUT>(A, st, L, pre); break;
+    case 2: mlp_forward<ACT, STD, 2, MIR, NOUT>(A, st, L, pre); break;
+    case 3: mlp_forward<ACT, STD, 3, MIR, NOUT>(A, st, L, pre); break;
+    default: mlp_forward<ACT, STD, 0, MIR, NOUT>(A, st, L, pre); break;
   }
 }
 
@@ -610,8 +629,10 @@ __device__ __forceinline__ void run_mlp_generic(const vbn_walk_args& A, const vb
   }
 }
 
-// KM bit 5: some NN CPD uses a non-relu activation; bit 6: half-wave instantiation.  ``pre``: the step's draws (see mlp_forward).
-template <unsigned KM, typename F>
+// KM bit 5: some NN CPD uses a non-relu activation; bit 6: half-wave instantiation.  ``pre``:
+// the step's draws (see mlp_forward).  NOUT > 0: the caller's head width is a compile-time
+// constant (gaussian_nn with D = 1: loc, scale).
+template <unsigned KM, int NOUT = 0, typename F>
 __device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
   constexpr bool MIR = (KM & 64) != 0;             // half-wave instantiation
   if constexpr ((KM & 512) != 0) {                 // kind-set bit 9: plans with generic MLPs
@@ -623,17 +644,18 @@ __device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& 
   }
   const bool sd = (st.flags & VBN_F_STANDARDIZE) != 0;
   if (!(KM & 32) || st.act == VBN_ACT_RELU) {
-    if (sd) mlp_nin<VBN_ACT_RELU, true, MIR>(A, st, L, pre); else mlp_nin<VBN_ACT_RELU, false, MIR>(A, st, L, pre);
+    if (sd) mlp_nin<VBN_ACT_RELU, true, MIR, NOUT>(A, st, L, pre);
+    else mlp_nin<VBN_ACT_RELU, false, MIR, NOUT>(A, st, L, pre);
     return;
   }
   if constexpr ((KM & 32) != 0) {
     switch (st.act * 2 + (sd ? 1 : 0)) {
-      case 2: mlp_nin<VBN_ACT_TANH, false, MIR>(A, st, L, pre); break;
-      case 3: mlp_nin<VBN_ACT_TANH, true, MIR>(A, st, L, pre); break;
-      case 4: mlp_nin<VBN_ACT_GELU, false, MIR>(A, st, L, pre); break;
-      case 5: mlp_nin<VBN_ACT_GELU, true, MIR>(A, st, L, pre); break;
-      case 6: mlp_nin<VBN_ACT_ELU, false, MIR>(A, st, L, pre); break;
-      default: mlp_nin<VBN_ACT_ELU, true, MIR>(A, st, L, pre); break;
+      case 2: mlp_nin<VBN_ACT_TANH, false, MIR, NOUT>(A, st, L, pre); break;
+      case 3: mlp_nin<VBN_ACT_TANH, true, MIR, NOUT>(A, st, L, pre); break;
+      case 4: mlp_nin<VBN_ACT_GELU, false, MIR, NOUT>(A, st, L, pre); break;
+      case 5: mlp_nin<VBN_ACT_GELU, true, MIR, NOUT>(A, st, L, pre); break;
+      case 6: mlp_nin<VBN_ACT_ELU, false, MIR, NOUT>(A, st, L, pre); break;
+      default: mlp_nin<VBN_ACT_ELU, true, MIR, NOUT>(A, st, L, pre); break;
     }
   }
 }
@@ -678,12 +700,9 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
     return;
   }
   float eps0 = 0.f;                                 // dim-0 draw, issued beside the weight loads
-#ifdef VBN_LATE_DRAW
-  run_mlp<KM>(A, st, L, [] {});
-  if (latent) eps0 = draw_normal(A, st, 0, L);
-#else
-  run_mlp<KM>(A, st, L, [&]() { if (latent) eps0 = draw_normal(A, st, 0, L); });
-#endif
+  auto pre = [&]() { if (latent) eps0 = draw_normal(A, st, 0, L); };
+  if (D == 1) run_mlp<KM, 2>(A, st, L, pre);        // head = (loc, raw scale): straight-line
+  else run_mlp<KM>(A, st, L, pre);
   const float min_scale = t[2 * D];
   float acc = 0.f;
   for (int d = 0; d < D; ++d) {
