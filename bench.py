@@ -205,6 +205,9 @@ def main():
     ap.add_argument("--prune-barren", action="store_true")
     ap.add_argument("--exact-f32", action="store_true", help="hidden layer on the exact f32 MFMA chain")
     ap.add_argument("--kde-valu", action="store_true", help="KDE distances on packed VALU (default: 16x16x4 f32 MFMA tile)")
+    ap.add_argument("--plan-jit", choices=("auto", "on", "off"), default="auto",
+                    help="plan-specialised walk kernel (hiprtc, vectorizedbayesiannetwork_amd/jit.py) or the "
+                         "step-table interpreter")
     args = ap.parse_args()
     if args.cpu_baseline_child:                       # fresh process, never touches the GPU
         cpu_baseline_child(args.config, args.cpu_queries, args.cpu_reps)
@@ -232,7 +235,8 @@ def main():
     B, S = cfg["B"], cfg["S"]                         # B = queries per GPU
     extra = {"n_particles": S} if cfg["engine"] == "rao_blackwellized_marginalization" else {}
     vbn.set_inference_method(cfg["engine"], n_samples=S, prune_barren=args.prune_barren,
-                             exact_f32=args.exact_f32, kde_valu=args.kde_valu, **extra)
+                             exact_f32=args.exact_f32, kde_valu=args.kde_valu,
+                             plan_jit={"auto": "auto", "on": True, "off": False}[args.plan_jit], **extra)
     engine = vbn._inference
     gather = not args.no_gather
     # every N the same path: shard the global batch, gather pdf / samples on rank 0 (async,
@@ -249,9 +253,13 @@ def main():
     # time is a steady-state figure and the chip's clocks have left their idle state before
     # the timed region (the first ~25 walks after idle run up to 17 % slower)
     from vectorizedbayesiannetwork_amd import engines as E
-    vbn.infer_posterior(query)                # builds the plan of the timed steps
+    from vectorizedbayesiannetwork_amd import jit, ops
+    t_first = time.perf_counter()
+    vbn.infer_posterior(query)                # builds (and compiles) the plan of the timed steps
     sharded.wait()
     torch.cuda.synchronize()
+    t_first = time.perf_counter() - t_first
+    specialised = bool(ops.LAST_WALK.get("specialised"))
     last = dict(E.LAST_LAUNCH)
     pk, plan, fixed = last["pk"], last["plan"], last["fixed"]
     stream = torch.cuda.current_stream()
@@ -272,6 +280,8 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize()
     kern_ms = ev0.elapsed_time(ev1) / reps
+    assert bool(ops.LAST_WALK.get("specialised")) == specialised, "kernel timing ran another walk form"
+    kernel_name = "vbn_walk_plan" if specialised else "vbn_walk_kernel"
 
     for _ in range(args.warmup):
         vbn.infer_posterior(query)
@@ -313,7 +323,7 @@ def main():
         # KDE: one exp per (particle, point) kernel weight; the bound is the v_exp_f32 issue rate
         ach = exps / kern_s / 1e12
         roof = {"bound": "exp", "achieved": round(ach, 4), "peak": round(EXP_PEAK_T, 2), "unit": "Texp/s",
-                "frac": round(ach / EXP_PEAK_T, 4), "traffic": traffic, "kernel": "vbn_walk_kernel",
+                "frac": round(ach / EXP_PEAK_T, 4), "traffic": traffic, "kernel": kernel_name,
                 "kernel_ms": round(kern_ms, 4), "exps_per_launch": exps,
                 "peak_basis": "v_exp_f32 issue: 8 cyc per wave64 per SIMD, 1024 SIMDs, 2.4 GHz",
                 "launches_timed": reps, "launches_untimed_before": untimed + 1}
@@ -324,7 +334,7 @@ def main():
         achieved = flops / kern_s / 1e12
         roof = {"bound": "mfma", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic,
-                "kernel": "vbn_walk_kernel", "kernel_ms": round(kern_ms, 4), "flops_per_launch": flops,
+                "kernel": kernel_name, "kernel_ms": round(kern_ms, 4), "flops_per_launch": flops,
                 "hidden_layer": "f32 MFMA" if exact else "split-f16 MFMA (3 pass, f32 accumulate)",
                 "peak_basis": f"f32 FLOPs at {FP32_PEAK_TFLOPS} TF, hidden-layer FLOPs at {hid_peak:.1f} TF",
                 "f32_equiv_frac_of_fp32_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
@@ -349,7 +359,11 @@ def main():
         "config": {"workload": f"{args.config}: {cfg['name']}", "queries_per_gpu": B, "global_batch": B * world,
                    "n_samples": S, "n_nodes": cfg["n_nodes"], "engine": cfg["engine"],
                    "parallelism": par, "gather": gather and dist, "prune_barren": args.prune_barren,
-                   "exact_f32": args.exact_f32, "kde_distances": "valu" if args.kde_valu else "mfma"},
+                   "exact_f32": args.exact_f32, "kde_distances": "valu" if args.kde_valu else "mfma",
+                   "walk": ("plan-specialised (step table compiled in with hiprtc)" if specialised
+                            else "step-table interpreter"),
+                   "plan_compile_s": round(jit.STATS["compile_s"], 2), "plan_cache_hits": jit.STATS["disk_hits"],
+                   "first_call_s": round(t_first, 2)},
         "roofline": roof,
     }
     if fallbacks:

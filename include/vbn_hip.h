@@ -41,13 +41,20 @@
 #ifndef VBN_HIP_H
 #define VBN_HIP_H
 
+#ifdef __HIPCC_RTC__               /* runtime compilation of plan-specialised walks (hiprtc) */
+using __hip_internal::int32_t;
+using __hip_internal::int64_t;
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#else
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 6
+#define VBN_ABI_VERSION 7
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001
@@ -179,6 +186,22 @@ int vbn_hip_struct_size(int which);
 
 /* Topological particle walk (see header comment). */
 int vbn_hip_walk(const vbn_walk_args* args, void* stream);
+
+/* The kind-set instantiation (walk_inst.hip / VBN_WALK_KIND_SETS: CPD kinds | 64 half-wave |
+ * 128 lean | 256 half-wave without injected draws | 512 generic MLP) vbn_hip_walk would launch
+ * for these arguments, or -(error code). */
+int vbn_hip_walk_kind_set(const vbn_walk_args* args);
+
+/* Plan-specialised walks.  A code object compiled at run time (hiprtc) from
+ * csrc/vbn_walk_plan.h for ONE step table and kind set -- the step fields, parent slots and
+ * LDS staging schedule as compile-time constants -- is loaded once and launched with the same
+ * arguments, grid and LDS as vbn_hip_walk; its outputs are bit-identical to vbn_hip_walk's.
+ * vbn_hip_walk_module refuses a launch whose kind set or step count differs from the
+ * module's.  (Replaces the same reference call sites as vbn_hip_walk.) */
+int vbn_hip_module_load(const void* code_object, const char* kernel_name, uint32_t kind_set, int32_t n_steps,
+                        void** handle);
+int vbn_hip_walk_module(const void* handle, const vbn_walk_args* args, void* stream);
+int vbn_hip_module_unload(void* handle);
 
 /* Per-query weight normalisation over S particles.
  *   normalize=1: w = softmax(log_w) per row, ess[b] = 1/sum(w^2)

@@ -6,6 +6,7 @@ on gfx950 FETCH_SIZE reads half the bytes of wide coalesced streaming reads (dou
 flagged as an upper estimate for other access widths); WRITE_SIZE is exact for 16-B
 streaming stores and uncalibrated for the walk's 4-B-per-lane stores (reported as is).
 Usage: summarize.py <prof_dir> <out.json> [kernel_substring]
+(default: the plan-specialised walk vbn_walk_plan when the trace has it, else vbn_walk_kernel)
 """
 import collections
 import csv
@@ -15,9 +16,12 @@ import sys
 
 def main():
     d, out = sys.argv[1], sys.argv[2]
-    kname = sys.argv[3] if len(sys.argv) > 3 else "vbn_walk_kernel"
-    res = {"kernel": kname}
     rows = list(csv.DictReader(open(f"{d}/trace/run_kernel_stats.csv")))
+    if len(sys.argv) > 3:
+        kname = sys.argv[3]
+    else:
+        kname = "vbn_walk_plan" if any("vbn_walk_plan" in r["Name"] for r in rows) else "vbn_walk_kernel"
+    res = {"kernel": kname}
     for r in rows:
         if kname in r["Name"]:
             res.update(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]), min_ns=float(r["MinNs"]),

@@ -1,0 +1,63 @@
+"""Plan-specialised walks (vectorizedbayesiannetwork_amd/jit.py, csrc/vbn_walk_plan.h) on
+the GPU: the step table compiled in as constants must give outputs bit-identical to the
+step-table interpreter (same device functions, same operation order, same Philox draws) for
+every engine and CPD family, so the lean parity tests (test_gpu_lean_parity.py, interpreter
+against the oracle) pin the specialised kernel too.  Each case compiles one plan with hiprtc
+(seconds; cached on disk for the rest of the session)."""
+from __future__ import annotations
+
+import pytest
+import torch
+
+from workloads import synthetic_workload
+
+pytestmark = pytest.mark.gpu
+
+B, S = 8, 1024
+
+
+def _engine(name, plan_jit):
+    from vectorizedbayesiannetwork_amd import engines as E
+    cls = {"mcm": E.MonteCarloMarginalization, "is": E.ImportanceSampling, "lw": E.LikelihoodWeighting,
+           "ancestral": E.AncestralSampler}[name]
+    return cls(n_samples=S, plan_jit=plan_jit)
+
+
+def _run(name, vbn, q, plan_jit, seed):
+    from vectorizedbayesiannetwork_amd import ops
+    eng = _engine(name, plan_jit)
+    out = eng.sample(vbn, q, S, seed=seed) if name == "ancestral" else eng.infer_posterior(vbn, q, seed=seed)
+    torch.cuda.synchronize()
+    out = out if isinstance(out, tuple) else (out,)
+    return [o.clone() for o in out], bool(ops.LAST_WALK.get("specialised"))
+
+
+@pytest.mark.parametrize("cfg_name,engine", [("cfg2", "mcm"), ("cfg2", "is"), ("cfg3", "is"), ("cfg3", "lw"),
+                                             ("cfg3", "ancestral"), ("cfg4", "mcm"), ("cfg5", "mcm")])
+def test_specialised_walk_bit_identical(cfg_name, engine):
+    from vectorizedbayesiannetwork_amd import jit
+    from vectorizedbayesiannetwork_amd.engines import Query
+    if not jit.enabled():
+        pytest.skip("VBN_PLAN_JIT=0")
+    model, vbn, target, ev = synthetic_workload(cfg_name, B, "cuda")
+    q = Query(target, {k: v.cuda() for k, v in ev.items()})
+    ref, spec_ref = _run(engine, vbn, q, False, seed=4242)
+    got, spec = _run(engine, vbn, q, True, seed=4242)
+    assert not spec_ref, "plan_jit=False must run the interpreter"
+    assert spec, f"plan_jit=True did not specialise ({jit._failed})"
+    for g, r in zip(got, ref):
+        assert g.shape == r.shape and torch.equal(torch.nan_to_num(g, 7.0, 8.0, 9.0), torch.nan_to_num(r, 7.0, 8.0, 9.0))
+        assert torch.equal(torch.isnan(g), torch.isnan(r))
+    # a second call reuses the loaded module (no recompile) and stays deterministic
+    again, spec2 = _run(engine, vbn, q, True, seed=4242)
+    assert spec2 and all(torch.equal(torch.nan_to_num(a, 7.0, 8.0, 9.0), torch.nan_to_num(g, 7.0, 8.0, 9.0))
+                         for a, g in zip(again, got))
+
+
+def test_auto_mode_keeps_small_launches_on_the_interpreter():
+    from vectorizedbayesiannetwork_amd import jit
+    from vectorizedbayesiannetwork_amd.engines import Query
+    model, vbn, target, ev = synthetic_workload("cfg2", B, "cuda")
+    q = Query(target, {k: v.cuda() for k, v in ev.items()})
+    _, spec = _run("mcm", vbn, q, "auto", seed=1)
+    assert B * S < jit.JIT_MIN_PARTICLES and not spec

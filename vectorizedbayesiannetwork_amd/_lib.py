@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -25,6 +25,10 @@ EXPORTS = (
     "vbn_hip_posterior_stats",
     "vbn_hip_lds_bytes",
     "vbn_hip_struct_size",
+    "vbn_hip_walk_kind_set",
+    "vbn_hip_module_load",
+    "vbn_hip_walk_module",
+    "vbn_hip_module_unload",
 )
 
 
@@ -115,6 +119,15 @@ def load(path: str = None) -> ctypes.CDLL:
         lib.vbn_hip_posterior_stats.restype = ctypes.c_int
         lib.vbn_hip_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
         lib.vbn_hip_lds_bytes.restype = ctypes.c_int64
+        lib.vbn_hip_walk_kind_set.argtypes = [ctypes.POINTER(VbnWalkArgs)]
+        lib.vbn_hip_walk_kind_set.restype = ctypes.c_int
+        lib.vbn_hip_module_load.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int32,
+                                            ctypes.POINTER(ctypes.c_void_p)]
+        lib.vbn_hip_module_load.restype = ctypes.c_int
+        lib.vbn_hip_walk_module.argtypes = [ctypes.c_void_p, ctypes.POINTER(VbnWalkArgs), ctypes.c_void_p]
+        lib.vbn_hip_walk_module.restype = ctypes.c_int
+        lib.vbn_hip_module_unload.argtypes = [ctypes.c_void_p]
+        lib.vbn_hip_module_unload.restype = ctypes.c_int
         lib.vbn_hip_struct_size.argtypes = [ctypes.c_int]
         lib.vbn_hip_struct_size.restype = ctypes.c_int
         if lib.vbn_hip_struct_size(0) != ctypes.sizeof(VbnWalkArgs) or lib.vbn_hip_struct_size(1) != 128:

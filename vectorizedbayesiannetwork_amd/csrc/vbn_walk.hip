@@ -304,7 +304,16 @@ extern "C" int64_t vbn_hip_lds_bytes(int32_t n_slots, int32_t max_out) {
   return (int64_t)(n_slots + (max_out > 0 ? max_out : 1)) * WAVE * (int64_t)sizeof(float);
 }
 
-extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
+// Launch shape and instantiation of one walk: validates the arguments, picks the smallest
+// instantiated kind set covering the plan and the workgroup size / LDS bytes (shared by the
+// interpreter launch and the plan-specialised module launch).
+struct walk_launch {
+  unsigned kmi;      // instantiated kind set (VBN_WALK_KIND_SETS)
+  dim3 grid, block;
+  size_t lds;
+};
+
+static int walk_shape(const vbn_walk_args* a, walk_launch* out) {
   if (!a || (!a->steps && a->n_steps > 0) || a->n_steps < 0 || !a->params || a->n_samples <= 0 ||
       a->n_queries <= 0 || a->n_slots <= 0)
     return fail(VBN_E_ARGS, "vbn_hip_walk: bad arguments");
@@ -325,7 +334,7 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   const bool generic = ((unsigned)a->kind_mask & 512u) != 0;   // some MLP with other hidden_dims
   if (generic) km = 63u;
 #ifdef VBN_KM_ONLY
-  km = VBN_KM_ONLY;
+  km = VBN_KM_ONLY & 63u;
 #endif
   // waves per workgroup: staged kind sets take the most resident waves per CU (160 KiB LDS,
   // 16 waves = 4 per SIMD at the kernel's register budget), larger workgroups on ties (one
@@ -366,30 +375,99 @@ extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
   const int64_t total = a->n_queries * (int64_t)a->n_samples;
   const int64_t blocks = (total + wp * nw - 1) / (wp * nw);
   if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
-  const dim3 grid((unsigned)blocks), block(WAVE * nw);
-  hipStream_t st = (hipStream_t)stream;
   // kind set | 64: the half-wave (mirror) instantiation; | 128: the lean one
   const bool lean = !a->noise && !a->state && a->mode != VBN_MODE_GIBBS;
-  const unsigned kmi = km | (wp == 32 ? 64u : 0u) | (lean && wp != 32 ? 128u : 0u) |
-                       (wp == 32 && !a->noise ? 256u : 0u) |  // | 256: half-wave without injected draws
-                       (generic ? 512u : 0u);                 // | 512: with the generic-MLP path
+  out->kmi = km | (wp == 32 ? 64u : 0u) | (lean && wp != 32 ? 128u : 0u) |
+             (wp == 32 && !a->noise ? 256u : 0u) |  // | 256: half-wave without injected draws
+             (generic ? 512u : 0u);                 // | 512: with the generic-MLP path
+  out->grid = dim3((unsigned)blocks);
+  out->block = dim3(WAVE * nw);
+  out->lds = (size_t)lds;
+  return 0;
+}
+
+extern "C" int vbn_hip_walk_kind_set(const vbn_walk_args* a) {
+  walk_launch w;
+  const int rc = walk_shape(a, &w);
+  return rc ? -rc : (int)w.kmi;
+}
+
+extern "C" int vbn_hip_walk(const vbn_walk_args* a, void* stream) {
+  walk_launch w;
+  const int rc = walk_shape(a, &w);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
   hipError_t e = hipErrorInvalidDeviceFunction;
 #ifdef VBN_KM_ONLY
   // experiment builds (make exp KM=...): one instantiation only
   // (a lean-less set may serve a lean launch; never the reverse)
+  const unsigned want = (unsigned)a->kind_mask & 63u;
+  const bool lean = (w.kmi & 128u) != 0;
+  const int64_t wp = a->wave_particles == 32 ? 32 : WAVE;
   if ((VBN_KM_ONLY & want) != want || ((VBN_KM_ONLY & 64) != 0) != (wp == 32) || ((VBN_KM_ONLY & 128) && !lean) ||
       ((VBN_KM_ONLY & 256) && a->noise))
     return fail(VBN_E_ARGS, "vbn_hip_walk: kind set not built in this experiment library");
-  (void)kmi;
-  e = VBN_LAUNCHER(VBN_KM_ONLY)(a, grid, block, (size_t)lds, st);
+  e = VBN_LAUNCHER(VBN_KM_ONLY)(a, w.grid, w.block, w.lds, st);
 #else
-  switch (kmi) {
-#define VBN_CASE(K) case K##u: e = vbn_launch_walk_km##K(a, grid, block, (size_t)lds, st); break;
+  switch (w.kmi) {
+#define VBN_CASE(K) case K##u: e = vbn_launch_walk_km##K(a, w.grid, w.block, w.lds, st); break;
     VBN_WALK_KIND_SETS(VBN_CASE)
 #undef VBN_CASE
     default: break;
   }
 #endif
+  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// plan-specialised walks: code objects compiled at run time (vbn_walk_plan.h)
+// ------------------------------------------------------------------------------------------
+struct vbn_plan_module {
+  hipModule_t mod;
+  hipFunction_t fn;
+  unsigned kmi;
+  int n_steps;
+};
+
+extern "C" int vbn_hip_module_load(const void* image, const char* kernel, uint32_t kind_set, int32_t n_steps,
+                                   void** handle) {
+  if (!image || !kernel || !handle) return fail(VBN_E_ARGS, "vbn_hip_module_load: bad arguments");
+  vbn_plan_module* m = new vbn_plan_module{};
+  hipError_t e = hipModuleLoadData(&m->mod, image);
+  if (e == hipSuccess) e = hipModuleGetFunction(&m->fn, m->mod, kernel);
+  if (e != hipSuccess) {
+    if (m->mod) hipModuleUnload(m->mod);
+    delete m;
+    return fail((int)e, hipGetErrorString(e));
+  }
+  m->kmi = kind_set;
+  m->n_steps = n_steps;
+  *handle = m;
+  return 0;
+}
+
+extern "C" int vbn_hip_module_unload(void* handle) {
+  vbn_plan_module* m = (vbn_plan_module*)handle;
+  if (!m) return 0;
+  const hipError_t e = hipModuleUnload(m->mod);
+  delete m;
+  return e == hipSuccess ? 0 : fail((int)e, hipGetErrorString(e));
+}
+
+extern "C" int vbn_hip_walk_module(const void* handle, const vbn_walk_args* a, void* stream) {
+  const vbn_plan_module* m = (const vbn_plan_module*)handle;
+  if (!m) return fail(VBN_E_ARGS, "vbn_hip_walk_module: no module");
+  walk_launch w;
+  const int rc = walk_shape(a, &w);
+  if (rc) return rc;
+  if (w.kmi != m->kmi || a->n_steps != m->n_steps)
+    return fail(VBN_E_ARGS, "vbn_hip_walk_module: the launch does not match the compiled plan (kind set / steps)");
+  vbn_walk_args args = *a;
+  const float* params = a->params;
+  void* kp[] = {&args, &params};
+  const hipError_t e = hipModuleLaunchKernel(m->fn, w.grid.x, 1, 1, w.block.x, 1, 1, (unsigned)w.lds,
+                                             (hipStream_t)stream, kp, nullptr);
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;
 }

@@ -24,6 +24,7 @@
 //   kde                  vbn/cpds/kde.py:105-182
 //   softmax_nn           vbn/cpds/softmax_nn.py:581-759
 //   softmax + ESS        importance_sampling.py:82-84, likelihood_weighting.py:75-80
+#ifndef __HIPCC_RTC__               // hiprtc (plan-specialised walks) brings its own runtime
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
@@ -31,8 +32,13 @@
 #include <string.h>
 
 #include <algorithm>
+#endif
 
 #include "vbn_hip.h"
+
+#ifndef INFINITY
+#define INFINITY __builtin_inff()
+#endif
 
 #define WAVE 64
 #define KDE_CHUNKS 16
@@ -1740,7 +1746,7 @@ __device__ __forceinline__ void stage_block(const vbn_walk_args& A, const vbn_st
 // first step >= j that runs an MLP (has a weight block), or -1
 __device__ __forceinline__ int first_mlp(const vbn_step* __restrict__ steps, int j, int n) {
   for (; j < n; ++j)
-    if (CI(steps)[j * (int)(sizeof(vbn_step) / 4) + (int)(offsetof(vbn_step, reserved) / 4) + 6] > 0) return j;
+    if (CI(steps)[j * (int)(sizeof(vbn_step) / 4) + (int)(__builtin_offsetof(vbn_step, reserved) / 4) + 6] > 0) return j;
   return -1;
 }
 

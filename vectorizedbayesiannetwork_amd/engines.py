@@ -189,9 +189,10 @@ def noise_tensor(pk: PackedModel, plan: QueryPlan, noise: Dict[str, Tuple], b: i
 def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: int, *,
              seed: int, offset: int = 0, q_base: int = 0, noise=None,
              fixed_per_particle: bool = False, state: Optional[torch.Tensor] = None, state_flags: int = 0,
-             step_begin: int = 0, step_end: int = -1) -> Tuple[torch.Tensor, torch.Tensor]:
+             step_begin: int = 0, step_end: int = -1, plan_jit: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
     """One launch of the particle walk; returns (lp [b,n] or empty, x [b,n,n_out_cols]).
-    ``state``/``state_flags``/``step_begin``/``step_end``: one segment of a split walk."""
+    ``state``/``state_flags``/``step_begin``/``step_end``: one segment of a split walk;
+    ``plan_jit``: ops.walk (0 interpreter, 1 plan-specialised for large lean launches, 2 always)."""
     n_out_cols = int(plan.out_cols.numel()) if plan.out_nodes else 0
     noise_b = 1
     if isinstance(noise, dict):
@@ -204,13 +205,13 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
         if noise.shape[3] != n or noise.shape[4] != pk.dmax:
             raise ValueError(f"noise must be [n_latent, 2, B|1, {n}, {pk.dmax}]")
     LAST_LAUNCH.update(pk=pk, plan=plan, fixed=fixed, b=b, n=n, fixed_per_particle=fixed_per_particle,
-                       noise=noise, state=state, seed=seed, offset=offset)
+                       noise=noise, state=state, seed=seed, offset=offset, plan_jit=plan_jit)
     args = (plan.steps, plan.in_cols, pk.params, fixed, noise, plan.out_cols, b, n,
             plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
             len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
             plan.mode != MODE_SAMPLE, plan.kind_mask)
     if state is None:
-        lp, x = ops.walk(*args, plan.wbuf)
+        lp, x = ops.walk(*args, plan.wbuf, plan_jit)
     else:
         lp, x = ops.walk_segment(*args, state, state_flags, step_begin, step_end, plan.wbuf)
     if plan.mode != MODE_SAMPLE:
@@ -222,8 +223,10 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
 
 class _EngineBase:
     def __init__(self, n_samples: int = 200, seed: Optional[int] = None, prune_barren: bool = False,
-                 q_base: int = 0, exact_f32: bool = False, kde_valu: bool = False, **kwargs):
+                 q_base: int = 0, exact_f32: bool = False, kde_valu: bool = False, plan_jit="auto", **kwargs):
         self.n_samples = int(n_samples)
+        # plan-specialised walks (jit.py): "auto" = large lean launches, True = every lean launch
+        self.plan_jit = 2 if plan_jit is True else (0 if plan_jit is False else 1)
         self.seed = seed
         self.prune_barren = bool(prune_barren)
         self.q_base = int(q_base)
@@ -288,7 +291,7 @@ class MonteCarloMarginalization(_EngineBase):
             b_eff = b
         fx = _fixed_buffer(plan, vals, b_eff, dev)
         pdf, xs = run_walk(pk, plan, fx, b_eff, n, seed=self._seed(kwargs), q_base=self.q_base,
-                           noise=kwargs.get("_noise"))
+                           noise=kwargs.get("_noise"), plan_jit=self.plan_jit)
         return pdf, xs
 
 
@@ -320,7 +323,8 @@ class LikelihoodWeighting(_EngineBase):
         seed = kwargs.get("_seed_value")
         if seed is None:
             seed = self._seed(kwargs)
-        log_w, xs = run_walk(pk, plan, fx, b, n, seed=seed, offset=offset, q_base=self.q_base, noise=noise)
+        log_w, xs = run_walk(pk, plan, fx, b, n, seed=seed, offset=offset, q_base=self.q_base, noise=noise,
+                             plan_jit=self.plan_jit)
         return log_w, xs
 
     def infer_posterior(self, vbn, query, **kwargs):
@@ -344,7 +348,8 @@ class ImportanceSampling(LikelihoodWeighting):
         self._last_fallback = False
         self._last_ess: Optional[torch.Tensor] = None
         self._lw = LikelihoodWeighting(n_samples=self.n_samples, q_base=self.q_base,
-                                       exact_f32=self.exact_f32, kde_valu=self.kde_valu)
+                                       exact_f32=self.exact_f32, kde_valu=self.kde_valu,
+                                       plan_jit={0: False, 1: "auto", 2: True}[self.plan_jit])
 
     def fallback_needed(self, ess: torch.Tensor, n: int) -> torch.Tensor:
         """Device-side flag (NaN ESS never triggers; importance_sampling.py:85-86)."""
@@ -386,7 +391,7 @@ def _descendants(model: BNModel, node: str) -> set:
 class RaoBlackwellizedMarginalization(_EngineBase):
     """rao_blackwellized_marginalization.py:15-324 on the GPU."""
 
-    _BASE_KW = ("seed", "prune_barren", "q_base", "exact_f32", "kde_valu")
+    _BASE_KW = ("seed", "prune_barren", "q_base", "exact_f32", "kde_valu", "plan_jit")
 
     def __init__(self, n_samples: int = 200, n_particles: Optional[int] = None, stddevs: float = 4.0,
                  min_scale: float = 1e-6, fallback: Optional[str] = "likelihood_weighting", **kwargs):
@@ -453,7 +458,7 @@ class RaoBlackwellizedMarginalization(_EngineBase):
                           skip=sorted(desc))
         fx = _fixed_buffer(plan, vals, b, dev)
         log_w, prm = run_walk(pk, plan, fx, b, n_part, seed=self._seed(kwargs), q_base=self.q_base,
-                              noise=kwargs.get("_noise"))
+                              noise=kwargs.get("_noise"), plan_jit=self.plan_jit)
         if mode == 0:
             z = torch.linspace(0.0, 1.0, n).to(dev)                                   # 304
             pdf, grid = ops.rb_epilogue(log_w, prm, z, n, 0, self.stddevs, self.min_scale, 1e-12)
@@ -506,7 +511,8 @@ class ResampledImportanceSampling(_EngineBase):
         # empty when the last node is evidence (it only reloads the state and writes outputs)
         cuts = ([i + 1 for i, x in enumerate(order) if x in ev] if resample else []) + [len(order)]
         if len(cuts) == 1:
-            log_w, xs = run_walk(pk, plan, fx, b, n, seed=seed, q_base=self.q_base, noise=noise)
+            log_w, xs = run_walk(pk, plan, fx, b, n, seed=seed, q_base=self.q_base, noise=noise,
+                                 plan_jit=self.plan_jit)
         else:
             total = b * n
             st_a = torch.empty(plan.n_slots + 1, total, device=dev, dtype=torch.float32)
@@ -557,7 +563,7 @@ class AncestralSampler(_EngineBase):
                      skip=[x for x in model.topo if x not in keep])
         fx = _fixed_buffer(plan, vals, b, dev)
         _, xs = run_walk(pk, plan, fx, b, n, seed=self._seed(kwargs), q_base=self.q_base,
-                         noise=kwargs.get("_noise"))
+                         noise=kwargs.get("_noise"), plan_jit=self.plan_jit)
         if target:
             return xs
         out, c = {}, 0

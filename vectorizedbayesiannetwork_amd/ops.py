@@ -44,12 +44,14 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
          out_cols: Tensor, n_queries: int, n_samples: int, n_slots: int, max_out: int,
          fixed_ld: int, fixed_per_particle: bool, noise_b: int, n_noise: int, dmax: int,
          n_out_cols: int, mode: int, q_base: int, seed: int, offset: int,
-         want_lp: bool, kind_mask: int = 63, wbuf: int = 0) -> Tuple[Tensor, Tensor]:
+         want_lp: bool, kind_mask: int = 63, wbuf: int = 0, plan_jit: int = 1) -> Tuple[Tensor, Tensor]:
     """One particle walk over the whole step table (``wbuf``: floats per LDS weight buffer,
-    >= every step's weight-block length)."""
+    >= every step's weight-block length).  ``plan_jit``: 0 = step-table interpreter, 1 = the
+    plan-specialised walk (jit.py) for lean launches of >= jit.JIT_MIN_PARTICLES particles,
+    2 = for every lean launch."""
     return _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots,
                         max_out, fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode,
-                        q_base, seed, offset, want_lp, kind_mask, None, 0, 0, -1, wbuf)
+                        q_base, seed, offset, want_lp, kind_mask, None, 0, 0, -1, wbuf, plan_jit)
 
 
 @torch.library.custom_op("vbn_hip::walk_segment", mutates_args=("state",))
@@ -89,7 +91,7 @@ def _check_wbuf(op: str, steps: Tensor, begin: int, end: int, wbuf: int) -> None
 
 def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                  fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
-                 offset, want_lp, kind_mask, state, state_flags, step_begin, step_end, wbuf):
+                 offset, want_lp, kind_mask, state, state_flags, step_begin, step_end, wbuf, plan_jit=0):
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::walk runs on the GPU only (no CPU fallback); "
@@ -151,14 +153,40 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
     a.wbuf_floats = int(wbuf)
     lib = _lib.load()
     with torch.cuda.device(device):
-        _lib.check(lib.vbn_hip_walk(ctypes.byref(a), ctypes.c_void_p(_stream_handle(device))), "vbn_hip_walk")
+        stream = ctypes.c_void_p(_stream_handle(device))
+        module = _plan_module(lib, a, steps, step_begin, step_end, total, plan_jit, device)
+        if module is not None:
+            _lib.check(lib.vbn_hip_walk_module(ctypes.c_void_p(module), ctypes.byref(a), stream), "vbn_hip_walk_module")
+        else:
+            _lib.check(lib.vbn_hip_walk(ctypes.byref(a), stream), "vbn_hip_walk")
+    LAST_WALK["specialised"] = module is not None
     return lp, x
+
+
+# how the last walk ran (bench.py / tests): {"specialised": bool}
+LAST_WALK = {"specialised": False}
+
+
+def _plan_module(lib, a, steps, step_begin, step_end, total, plan_jit, device):
+    """Module handle of the plan-specialised walk for this launch, or None (interpreter)."""
+    if not plan_jit or a.noise or a.state or a.mode == MODE_GIBBS or step_begin != 0 or step_end != steps.shape[0]:
+        return None
+    from . import jit
+    if not jit.enabled() or (plan_jit == 1 and total < jit.JIT_MIN_PARTICLES):
+        return None
+    host = getattr(steps, "_vbn_host", None)
+    if host is None:
+        return None
+    km = lib.vbn_hip_walk_kind_set(ctypes.byref(a))
+    if km <= 0 or not (km & 128) or (km & 64):          # lean full-wave launches only
+        return None
+    return jit.module_for(host[0], host[1], km, device.index if device.index is not None else 0, host[2])
 
 
 @walk.register_fake
 def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
-               offset, want_lp, kind_mask=63, wbuf=0):
+               offset, want_lp, kind_mask=63, wbuf=0, plan_jit=1):
     total = n_queries * n_samples
     lp = params.new_empty(total if want_lp else 0)
     x = params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))

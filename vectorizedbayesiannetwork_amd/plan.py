@@ -16,6 +16,7 @@ work is split in two device-resident objects:
 """
 from __future__ import annotations
 
+import hashlib
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -578,6 +579,10 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         max_out = max(max_out, KDE_CHUNKS)
     steps_t = torch.from_numpy(steps).to(dev) if len(order) else torch.zeros(1, STEP_INTS, dtype=torch.int32, device=dev)
     steps_t._vbn_wblk_max = int(steps[:, S_WBLK_LEN].max()) if len(order) else 0   # ops._check_wbuf
+    ic_host = np.asarray(in_cols, np.int32).reshape(-1)
+    # host copies for the plan-specialised walk (jit.py); the key names this exact table
+    steps_t._vbn_host = (steps.copy(), ic_host.copy(),
+                         hashlib.sha1(steps.tobytes() + b"|" + ic_host.tobytes()).hexdigest())
     return QueryPlan(
         steps=steps_t,
         in_cols=t(in_cols), out_cols=t(out_cols), n_steps=len(order), n_slots=max(n_slots, 1),
