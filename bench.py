@@ -186,7 +186,7 @@ def load_traffic(cfg_name: str):
         return None, None
 
 
-KT_UNTIMED, KT_TIMED = 20, 10     # roofline kernel timing: untimed launches, then timed ones
+KT_UNTIMED, KT_TIMED = 64, 20     # roofline kernel timing: untimed launches, then timed ones
 
 
 def main():
@@ -269,8 +269,9 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize()
     first_ms = max(ev0.elapsed_time(ev1), 1e-3)
-    # ~40 ms of untimed walks (the clock ramp), then >= 3 timed (~20 ms, at most 10)
-    untimed = max(2, min(KT_UNTIMED, math.ceil(40.0 / first_ms)))
+    # ~60 ms of untimed walks (the clock ramp: a 0.9-ms walk needs ~35 launches to reach its
+    # steady clock, profiles/r03_cfg2_kernel_trace), then >= 3 timed (~20 ms, at most 20)
+    untimed = max(2, min(KT_UNTIMED, math.ceil(60.0 / first_ms)))
     reps = max(3, min(KT_TIMED, math.ceil(20.0 / first_ms)))
     for i in range(untimed):
         E.run_walk(pk, plan, fixed, B, S, seed=1001 + i)

@@ -57,7 +57,10 @@ def main():
     ap.add_argument("--cpu-chains", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wave-particles", type=int, default=None, help="32 / 64 (default: the engine's choice)")
+    ap.add_argument("--plan-jit", choices=("auto", "on", "off"), default="auto",
+                    help="plan-specialised sweep kernel (vectorizedbayesiannetwork_amd/jit.py) or the interpreter")
     args = ap.parse_args()
+    pj = {"auto": "auto", "on": True, "off": False}[args.plan_jit]
     torch.cuda.set_device(0)
     cfg, model, vbn, query = Bm.build_workload("cfg2", "cuda:0", 1)
     B = args.chains
@@ -65,7 +68,7 @@ def main():
     query = {"target": query["target"],
              "evidence": {k: v.repeat(reps_ev, 1)[:B].contiguous() for k, v in query["evidence"].items()}}
     vbn.set_sampling_method("gibbs", n_samples=args.n_samples, burn_in=args.burn_in, n_steps=args.thin, seed=1,
-                            wave_particles=args.wave_particles)
+                            wave_particles=args.wave_particles, plan_jit=pj)
     for _ in range(args.warmup):
         vbn.sample(query, n_samples=args.n_samples)
     torch.cuda.synchronize()
@@ -91,8 +94,9 @@ def main():
     def launch(seed):
         return ops.gibbs_walk(gp.steps, gp.in_cols, pk.params, fx, None, state, B, gp.init.n_slots,
                               gp.init.max_out, gp.init.fixed_ld, B, gp.n_noise, pk.dmax, 1, iters, iters - 1, 1,
-                              0, seed, 1, gp.kind_mask, gp.wbuf, wp)
+                              0, seed, 1, gp.kind_mask, gp.wbuf, wp, eng.plan_jit)
     launch(0)
+    specialised = bool(ops.LAST_WALK.get("specialised"))
     stream = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 3
@@ -116,9 +120,10 @@ def main():
         "data": "synthetic (cfg2 DAG/SEM/query generator; random-init CPD weights)",
         "config": {"workload": "gibbs32: 32node-gaussian_nn-gibbs", "chains": B, "n_samples": args.n_samples,
                    "burn_in": args.burn_in, "n_steps": args.thin, "sweeps": iters, "candidates": 8,
-                   "wave_particles": wp},
+                   "wave_particles": wp,
+                   "walk": "plan-specialised" if specialised else "step-table interpreter"},
         "roofline": {"bound": "mfma", "achieved": round(ach, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
-                     "frac": round(ach / peak, 4), "traffic": None, "kernel": "vbn_walk_kernel (GIBBS)",
+                     "frac": round(ach / peak, 4), "traffic": None, "kernel": ("vbn_walk_plan" if specialised else "vbn_walk_kernel") + " (GIBBS)",
                      "kernel_ms": round(kern_ms, 3), "flops_per_launch": f32 + hid,
                      "sweep_lane_evals_per_s": round(lanes / (kern_ms * 1e-3), 1), "launches_timed": reps},
     }

@@ -61,3 +61,27 @@ def test_auto_mode_keeps_small_launches_on_the_interpreter():
     q = Query(target, {k: v.cuda() for k, v in ev.items()})
     _, spec = _run("mcm", vbn, q, "auto", seed=1)
     assert B * S < jit.JIT_MIN_PARTICLES and not spec
+
+
+@pytest.mark.parametrize("wave_particles", [32, 64])
+def test_specialised_gibbs_sweeps_bit_identical(wave_particles):
+    """Gibbs sweeps (non-lean form, chain state resumed from the start walk, the sweep loop
+    around the compile-time table, LDS staging across the sweep boundary), half- and
+    full-wave: the chains equal the interpreter's bit for bit."""
+    from vectorizedbayesiannetwork_amd import jit, ops
+    from vectorizedbayesiannetwork_amd.engines import GibbsSampler, Query
+    if not jit.enabled():
+        pytest.skip("VBN_PLAN_JIT=0")
+    model, vbn, target, ev = synthetic_workload("cfg2", 16, "cuda")
+    q = Query(target, {k: v.cuda() for k, v in ev.items()})
+    outs = []
+    for pj in (False, True):
+        eng = GibbsSampler(n_samples=6, burn_in=3, n_steps=2, collect="chain", wave_particles=wave_particles,
+                           plan_jit=pj)
+        xs = eng.sample(vbn, q, 6, seed=99)
+        torch.cuda.synchronize()
+        outs.append((xs.clone(), bool(ops.LAST_WALK.get("specialised"))))
+    (ref, s0), (got, s1) = outs
+    assert not s0 and s1, f"specialisation flags {s0}, {s1} ({jit._failed})"
+    assert got.shape == ref.shape and torch.isfinite(ref).all()
+    assert torch.equal(got, ref)

@@ -661,7 +661,7 @@ class GibbsSampler(_EngineBase):
         out = ops.gibbs_walk(gp.steps, gp.in_cols, pk.params, fx,
                              sweep_noise, chains.contiguous(), b, init.n_slots, init.max_out, init.fixed_ld,
                              noise_b, gp.n_noise, pk.dmax, dt, iters, burn, th, self.q_base, seed, 1,
-                             gp.kind_mask, gp.wbuf, self._wave_particles(b))
+                             gp.kind_mask, gp.wbuf, self._wave_particles(b), self.plan_jit)
         if self.collect == "chain" and n > 0:
             return out
         return out.expand(b, max(n, 1), dt).contiguous()

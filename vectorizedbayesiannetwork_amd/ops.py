@@ -167,18 +167,20 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
 LAST_WALK = {"specialised": False}
 
 
-def _plan_module(lib, a, steps, step_begin, step_end, total, plan_jit, device):
-    """Module handle of the plan-specialised walk for this launch, or None (interpreter)."""
-    if not plan_jit or a.noise or a.state or a.mode == MODE_GIBBS or step_begin != 0 or step_end != steps.shape[0]:
+def _plan_module(lib, a, steps, step_begin, step_end, work, plan_jit, device):
+    """Module handle of the plan-specialised walk for this launch, or None (interpreter).
+    ``work`` = particles x sweeps; ``plan_jit`` 1 (auto: launches without injected draws of at
+    least jit.JIT_MIN_PARTICLES particle-steps) or 2 (always)."""
+    if not plan_jit or step_begin != 0 or step_end != steps.shape[0]:
         return None
     from . import jit
-    if not jit.enabled() or (plan_jit == 1 and total < jit.JIT_MIN_PARTICLES):
+    if not jit.enabled() or (plan_jit == 1 and (a.noise or work < jit.JIT_MIN_PARTICLES)):
         return None
     host = getattr(steps, "_vbn_host", None)
     if host is None:
         return None
     km = lib.vbn_hip_walk_kind_set(ctypes.byref(a))
-    if km <= 0 or not (km & 128) or (km & 64):          # lean full-wave launches only
+    if km <= 0:
         return None
     return jit.module_for(host[0], host[1], km, device.index if device.index is not None else 0, host[2])
 
@@ -197,10 +199,12 @@ def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samp
 def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: Optional[Tensor],
                state: Tensor, n_queries: int, n_slots: int, max_out: int, fixed_ld: int, noise_b: int,
                n_noise: int, dmax: int, out_dim: int, iters: int, burn_in: int, thin: int, q_base: int,
-               seed: int, offset: int, kind_mask: int, wbuf: int = 0, wave_particles: int = 64) -> Tensor:
+               seed: int, offset: int, kind_mask: int, wbuf: int = 0, wave_particles: int = 64,
+               plan_jit: int = 1) -> Tensor:
     """``iters`` Gibbs sweeps (gibbs.py:34-87) over B chains x 8 candidate lanes, started from
     ``state`` [n_slots + 1, B*8]; returns the collected target values [B, n_collect, out_dim].
-    ``wave_particles`` 32: half-wave launch (4 chains per wave64, include/vbn_hip.h)."""
+    ``wave_particles`` 32: half-wave launch (4 chains per wave64, include/vbn_hip.h).
+    ``plan_jit`` as for :func:`walk` (0 interpreter, 1 auto, 2 always specialised)."""
     if wave_particles not in (32, 64):
         raise ValueError(f"vbn_hip::gibbs_walk: wave_particles must be 32 or 64, got {wave_particles}")
     device = params.device
@@ -262,14 +266,20 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
     a.wave_particles = int(wave_particles)
     lib = _lib.load()
     with torch.cuda.device(device):
-        _lib.check(lib.vbn_hip_walk(ctypes.byref(a), ctypes.c_void_p(_stream_handle(device))), "vbn_hip_walk")
+        stream = ctypes.c_void_p(_stream_handle(device))
+        module = _plan_module(lib, a, steps, 0, int(steps.shape[0]), total * iters, plan_jit, device)
+        if module is not None:
+            _lib.check(lib.vbn_hip_walk_module(ctypes.c_void_p(module), ctypes.byref(a), stream), "vbn_hip_walk_module")
+        else:
+            _lib.check(lib.vbn_hip_walk(ctypes.byref(a), stream), "vbn_hip_walk")
+    LAST_WALK["specialised"] = module is not None
     return x
 
 
 @gibbs_walk.register_fake
 def _gibbs_walk_fake(steps, in_cols, params, fixed, noise, state, n_queries, n_slots, max_out, fixed_ld,
                      noise_b, n_noise, dmax, out_dim, iters, burn_in, thin, q_base, seed, offset, kind_mask, wbuf=0,
-                     wave_particles=64):
+                     wave_particles=64, plan_jit=1):
     return params.new_empty((n_queries, (iters - burn_in + thin - 1) // thin, out_dim))
 
 

@@ -679,6 +679,9 @@ def build_gibbs_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Seque
     tab[sel, S_WBLK_LEN] = 0
     steps = torch.from_numpy(tab).to(packed.device)
     steps._vbn_wblk_max = int(tab[:, S_WBLK_LEN].max())                  # ops._check_wbuf
+    ic_host = full.steps._vbn_host[1]
+    steps._vbn_host = (tab.copy(), ic_host.copy(),                         # jit.py (sweep kernels)
+                       hashlib.sha1(b"gibbs|" + tab.tobytes() + b"|" + ic_host.tobytes()).hexdigest())
     return GibbsPlan(init=init, steps=steps, n_steps=len(table), latent=lat, target=target,
                      n_noise=max(2 * len(lat), 1), in_cols=full.in_cols, kind_mask=full.kind_mask,
                      wbuf=int(tab[:, S_WBLK_LEN].max()))
