@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Compile plan-specialised code objects of a bench workload's walk with extra options (A/B
+experiments for scripts/jit_ab.py; CPU only, hiprtc).
+
+    python scripts/jit_variants.py --config cfg3 base= wpe3=-DVBN_WPE=3 sb=-DVBN_PLAN_SCHED_BARRIER
+writes exp/plan_<config>_<name>.hsaco and prints the register usage of each.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("variants", nargs="+", help="name=space-separated extra options")
+    a = ap.parse_args()
+    import bench
+    from vectorizedbayesiannetwork_amd import jit
+    from vectorizedbayesiannetwork_amd.plan import MODE_MCM, MODE_WEIGHTED, PackedModel, build_plan
+    cfg, model, target, ev = bench.build_model(a.config)
+    pk = PackedModel(model, "cpu")
+    vals = set(ev)
+    lat = [x for x in model.topo if x not in vals]
+    fix = [x for x in model.topo if x in vals]
+    if cfg["engine"] == "importance_sampling":
+        plan = build_plan(pk, latent=lat, fixed=fix, logp=fix, out_nodes=[target], shared_roots=False,
+                          mode=MODE_WEIGHTED)
+    else:
+        plan = build_plan(pk, latent=lat, fixed=fix, logp=[target], out_nodes=[target], shared_roots=True,
+                          mode=MODE_MCM)
+    km = plan.kind_mask | 128
+    steps, ic, _ = plan.steps._vbn_host
+    src = jit.plan_source(steps, ic, km)
+    os.makedirs(os.path.join(REPO, "exp"), exist_ok=True)
+    base = jit.OPTIONS
+    for v in a.variants:
+        name, _, opts = v.partition("=")
+        jit.OPTIONS = tuple(base) + tuple(opts.split())
+        t0 = time.perf_counter()
+        code = jit.compile_source(src)
+        out = os.path.join(REPO, "exp", f"plan_{a.config}_{name}.hsaco")
+        with open(out, "wb") as f:
+            f.write(code)
+        print(f"{out}: kind set {km}, {len(code)} B, {time.perf_counter() - t0:.1f} s")
+    jit.OPTIONS = base
+
+
+if __name__ == "__main__":
+    main()

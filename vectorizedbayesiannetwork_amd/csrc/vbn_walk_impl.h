@@ -529,7 +529,18 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
   } else {
     mlp_head<ACT>(st, L, W, h0, h1, nan_in);
   }
+#ifdef VBN_SGB   // experiment: pin VBN_SGB VALU fillers behind each MFMA of the node's region
+#pragma unroll
+  for (int i = 0; i < VBN_SGB_N; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x002, VBN_SGB, 0);
+  }
+#endif
+#ifdef VBN_ABL_NOEXACT   // measurement only (wrong when the exact path is needed)
+  if (false) {
+#else
   if (big || (st.flags & VBN_F_F32L2)) {          // rare: the exact f32 chain, outputs overwritten
+#endif
     const float* __restrict__ Wg = L.P + WBLK_OFF(st);
     float y[16];
     mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 0, y, [] {});
