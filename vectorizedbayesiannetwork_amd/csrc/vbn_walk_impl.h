@@ -437,35 +437,46 @@ __device__ __forceinline__ void mlp_head(const vbn_step& st, const Lane& L, cons
 // Layer 1 of group g (v_mfma_f32_32x32x2_f32, K = n_in, bias rows as the accumulator init)
 // and its activation.  W = weight block base (LDS: staged block; global: blob + wblk_off), so
 // W1 sits at W[t * 64 + lane] and the biases at W + (off_b2 - wblk_off).  ``pre`` runs between
-// the fragment reads and the first MFMA (group 0: the step's draws).  Returns true
-// (wave-uniform) when some activation leaves the f16 split range |y| <= 32768 (NaN with the
-// sign bit clear counts as out of range).
-template <int ACT, bool STD, int NIN, typename F>
+// the fragment reads and the first MFMA (group 0: the step's draws).  Returns a wave-uniform
+// flag: CHK = 0 (fast path) -- some layer-1 operand lies beyond the node's bound zlim
+// (VBN_ZLIM: within it no activation can leave the f16 split range, plan._pack_mlp), one
+// compare per MFMA operand instead of one max per activation; CHK = 1 -- some activation
+// leaves the split range |y| <= 32768 (NaN with the sign bit clear counts as out of range).
+#define VBN_ZLIM(st) __int_as_float((st).reserved[1])
+template <int ACT, bool STD, int NIN, int CHK = 0, typename F>
 __device__ __forceinline__ bool mlp_l1_act(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
                                            const float* __restrict__ W, int g, float (&y)[16], F&& pre) {
   const int lane = L.lane;
   f32x16 a = load_acc16(W + (st.off_b2 - WBLK_OFF(st)) + 32 * g + 16 * (lane >> 5));
+  const float zlim = VBN_ZLIM(st);
+  bool out = false;
   if (NIN > 0) {
     float w1[(NIN + 1) / 2 > 0 ? (NIN + 1) / 2 : 1];
 #pragma unroll
     for (int t = 0; t < (NIN + 1) / 2; ++t) w1[t] = W[t * WAVE + lane];
     pre();
 #pragma unroll
-    for (int t = 0; t < (NIN + 1) / 2; ++t)
-      a = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[t], l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
+    for (int t = 0; t < (NIN + 1) / 2; ++t) {
+      const float op = l1_operand<STD, NIN>(A, st, L, t, g);
+      if (CHK == 0) out |= !(fabsf(op) <= zlim);
+      a = __builtin_amdgcn_mfma_f32_32x32x2f32(w1[t], op, a, 0, 0, 0);
+    }
   } else {
     pre();
     const int t1 = (st.n_in + 1) >> 1;
-    for (int t = 0; t < t1; ++t)
-      a = __builtin_amdgcn_mfma_f32_32x32x2f32(W[t * WAVE + lane], l1_operand<STD, NIN>(A, st, L, t, g), a, 0, 0, 0);
+    for (int t = 0; t < t1; ++t) {
+      const float op = l1_operand<STD, NIN>(A, st, L, t, g);
+      if (CHK == 0) out |= !(fabsf(op) <= zlim);
+      a = __builtin_amdgcn_mfma_f32_32x32x2f32(W[t * WAVE + lane], op, a, 0, 0, 0);
+    }
   }
   int big = 0;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     y[r] = act_fn<ACT>(a[r]);
-    big = max(big, __float_as_int(y[r]));        // activations are >= -1: only the positive side
+    if (CHK == 1) big = max(big, __float_as_int(y[r]));   // activations are >= -1: the positive side
   }
-  return __any(big > 0x47000000);
+  return CHK == 1 ? __any(big > 0x47000000) : __any(out);
 }
 
 // Head outputs with a compile-time count (NOUT > 0): straight-line code, so the scheduler can
@@ -502,17 +513,17 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
     nan_in |= (v != v);
   }
   f32x16 h0, h1;
-  bool big;
+  bool beyond;                                    // some layer-1 operand beyond the node's bound
   {
     float y[16];
-    big = mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 0, y, pre);
+    beyond = mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 0, y, pre);
     const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
     h0 = layer2_split(wq, load_acc16(b2), y);
     if constexpr (MIR) {
       h1 = h0;                                    // group 1 = group 0's particles
     } else {
       float y1[16];
-      big |= mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 1, y1, [] {});
+      beyond |= mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 1, y1, [] {});
       h1 = layer2_split(wq, load_acc16(b2 + 32), y1);
     }
   }
@@ -529,29 +540,28 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
   } else {
     mlp_head<ACT>(st, L, W, h0, h1, nan_in);
   }
-#ifdef VBN_SGB   // experiment: pin VBN_SGB VALU fillers behind each MFMA of the node's region
-#pragma unroll
-  for (int i = 0; i < VBN_SGB_N; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x002, VBN_SGB, 0);
-  }
-#endif
-#ifdef VBN_ABL_NOEXACT   // measurement only (wrong when the exact path is needed)
-  if (false) {
-#else
-  if (big || (st.flags & VBN_F_F32L2)) {          // rare: the exact f32 chain, outputs overwritten
-#endif
+  // rare: an operand beyond the bound -- check the activations themselves (recomputed from the
+  // blob: the same values); beyond the split range, the exact f32 chain overwrites the outputs
+  if (beyond || (st.flags & VBN_F_F32L2)) {
     const float* __restrict__ Wg = L.P + WBLK_OFF(st);
-    float y[16];
-    mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 0, y, [] {});
-    h0 = layer2_exact(st, L, 0, y);
-    if constexpr (MIR) {
-      h1 = h0;
-    } else {
-      mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 1, y, [] {});
-      h1 = layer2_exact(st, L, 1, y);
+    bool big = (st.flags & VBN_F_F32L2) != 0;
+    if (!big) {
+      float y[16];
+      big = mlp_l1_act<ACT, STD, NIN, 1>(A, st, L, Wg, 0, y, [] {});
+      if constexpr (!MIR) big |= mlp_l1_act<ACT, STD, NIN, 1>(A, st, L, Wg, 1, y, [] {});
     }
-    mlp_head<ACT>(st, L, W, h0, h1, nan_in);
+    if (big) {                                    // the exact f32 chain, outputs overwritten
+      float y[16];
+      mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 0, y, [] {});
+      h0 = layer2_exact(st, L, 0, y);
+      if constexpr (MIR) {
+        h1 = h0;
+      } else {
+        mlp_l1_act<ACT, STD, NIN>(A, st, L, Wg, 1, y, [] {});
+        h1 = layer2_exact(st, L, 1, y);
+      }
+      mlp_head<ACT>(st, L, W, h0, h1, nan_in);
+    }
   }
 }
 

@@ -94,9 +94,6 @@ __device__ __forceinline__ void vbn_plan_step_lean(const vbn_walk_args& A, const
   } else {
     L.wb = params + st.reserved[5];
   }
-#ifdef VBN_PLAN_SCHED_BARRIER   // experiment: no instruction motion across step boundaries
-  __builtin_amdgcn_sched_barrier(0);
-#endif
   walk_step<KM>(A, st, L, lp);
 }
 

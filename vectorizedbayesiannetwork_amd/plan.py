@@ -206,6 +206,16 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     # weights beyond the f16 split range: the node always takes the exact f32 layer-2 chain
     # (the split fragments are still packed, so the weight block layout does not change)
     offs["f32l2"] = int(np.abs(w2).max() > 32768.0)
+    # layer-1 operand bound (csrc mlp_l1_act): with every operand |x| <= zlim, each layer-1
+    # pre-activation |z| <= max|b1| + zlim max_r sum_k |W1[r, k]| and |act(z)| <= max(|z|, 1)
+    # stay inside the f16 split range, so the walk compares the operands (one per MFMA) instead
+    # of every activation; 0.1 % margin for the f32 accumulation.  -1: no bound (always check)
+    rs = float(np.abs(w1.astype(np.float64)).sum(axis=1).max()) if w1.size else 0.0
+    room = 32768.0 * (1.0 - 1e-3) - float(np.abs(b1.astype(np.float64)).max())
+    if room <= 1.0:
+        offs["zlim"] = -1.0
+    else:
+        offs["zlim"] = float(np.float32(min(room / rs, 3.0e38))) if rs > 0 else 3.0e38
     j = np.arange(8)
     frag = np.zeros((2, 64, 8), np.float32)
     for s in range(2):
@@ -548,6 +558,8 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
                          ("w2h", S_OFF_W2H)):
             row[idx] = npk.offs.get(key, 0)
         row[S_OFF_KQ] = npk.offs.get("kq", -1)
+        if "zlim" in npk.offs:                   # NN steps: layer-1 operand bound (f32 bits)
+            row[S_OFF_KQ] = np.float32(npk.offs["zlim"]).view(np.int32)
         row[S_OFF_KQY] = npk.offs.get("kqy", -1)
         row[S_OFF_KR] = npk.offs.get("kr", -1)
         row[S_OFF_KV] = npk.offs.get("kv", -1)
