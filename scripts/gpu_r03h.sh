@@ -8,7 +8,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -rs -x --timeout 300 --tim
 tail -5 gpurun_out/r03h_pytest_gpu.txt
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u scripts/jit_ab.py --config cfg2 exp/plan_cfg2_base.hsaco exp/plan_cfg2_zb.hsaco > gpurun_out/r03h_ab_cfg2.txt 2>&1 || exit 1
-timeout -k 10 300 python -u scripts/jit_ab.py --config cfg3 exp/plan_cfg3_base.hsaco exp/plan_cfg3_zb.hsaco > gpurun_out/r03h_ab_cfg3.txt 2>&1 || exit 1
+timeout -k 10 300 python -u scripts/jit_ab.py --config cfg3 exp/plan_cfg3_base.hsaco exp/plan_cfg3_zb.hsaco exp/plan_cfg3_zbrcp.hsaco exp/plan_cfg3_sel.hsaco exp/plan_cfg3_selrcp.hsaco > gpurun_out/r03h_ab_cfg3.txt 2>&1 || exit 1
 grep variant gpurun_out/r03h_ab_cfg2.txt gpurun_out/r03h_ab_cfg3.txt
 timeout -k 10 600 python -u bench.py > gpurun_out/r03h_bench_cfg2.json 2>gpurun_out/r03h_bench_cfg2.err || exit 1
 cat gpurun_out/r03h_bench_cfg2.json

@@ -14,13 +14,18 @@ import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "scripts"))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--gibbs", action="store_true",
+                    help="the Gibbs sweep table of scripts/jit_ab_gibbs.py (half-wave kind set 321)")
     ap.add_argument("variants", nargs="+", help="name=space-separated extra options")
     a = ap.parse_args()
+    if a.gibbs:
+        return gibbs_variants(a.variants)
     import bench
     from vectorizedbayesiannetwork_amd import jit
     from vectorizedbayesiannetwork_amd.plan import MODE_MCM, MODE_WEIGHTED, PackedModel, build_plan
@@ -46,6 +51,31 @@ def main():
         t0 = time.perf_counter()
         code = jit.compile_source(src)
         out = os.path.join(REPO, "exp", f"plan_{a.config}_{name}.hsaco")
+        with open(out, "wb") as f:
+            f.write(code)
+        print(f"{out}: kind set {km}, {len(code)} B, {time.perf_counter() - t0:.1f} s")
+    jit.OPTIONS = base
+
+
+def gibbs_variants(variants):
+    import bench
+    from vectorizedbayesiannetwork_amd import jit
+    from vectorizedbayesiannetwork_amd.plan import PackedModel, build_gibbs_plan
+    cfg, model, target, ev = bench.build_model("cfg2")
+    pk = PackedModel(model, "cpu")
+    vals = set(ev)
+    gp = build_gibbs_plan(pk, latent=[x for x in model.topo if x not in vals],
+                          fixed=[x for x in model.topo if x in vals], target=target)
+    steps, ic, _ = gp.steps._vbn_host
+    km = gp.kind_mask | 64 | 256            # half-wave, no injected draws (4096 chains)
+    src = jit.plan_source(steps, ic, km)
+    base = jit.OPTIONS
+    for v in variants:
+        name, _, opts = v.partition("=")
+        jit.OPTIONS = tuple(base) + tuple(opts.split())
+        t0 = time.perf_counter()
+        code = jit.compile_source(src)
+        out = os.path.join(REPO, "exp", f"gibbs_{name}.hsaco")
         with open(out, "wb") as f:
             f.write(code)
         print(f"{out}: kind set {km}, {len(code)} B, {time.perf_counter() - t0:.1f} s")

@@ -542,7 +542,11 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
   }
   // rare: an operand beyond the bound -- check the activations themselves (recomputed from the
   // blob: the same values); beyond the split range, the exact f32 chain overwrites the outputs
+#ifdef VBN_ABL_NOEXACT   // measurement only: no exact-path branch (wrong when it is needed)
+  if (false) {
+#else
   if (beyond || (st.flags & VBN_F_F32L2)) {
+#endif
     const float* __restrict__ Wg = L.P + WBLK_OFF(st);
     bool big = (st.flags & VBN_F_F32L2) != 0;
     if (!big) {
@@ -839,6 +843,26 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
       eps0 = draw_normal(A, st, 0, L);
     }
   };
+  // pi = softmax(logits).clamp_min(1e-5); pi /= sum (mdn.py:227-228), computed once per
+  // particle into the logit rows (the inverse CDF and the log-prob read pi_k repeatedly).
+  // The two normalisations multiply by one reciprocal each (within an ulp of the reference's
+  // divisions; cfg3 walk -1.8 %)
+  auto make_pi = [&]() {
+    lmax = -INFINITY;
+    for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, scr[k * WAVE + lane]);
+    lsum = 0.f;
+    for (int k = 0; k < K; ++k) lsum += __expf(scr[k * WAVE + lane] - lmax);
+    psum = 0.f;
+    const float rl = 1.0f / lsum;
+    for (int k = 0; k < K; ++k) {
+      const float p = fmaxf(__expf(scr[k * WAVE + lane] - lmax) * rl, 1e-5f);
+      scr[k * WAVE + lane] = p;
+      psum += p;
+    }
+    psum = fmaxf(psum, 1e-12f);
+    const float rp = 1.0f / psum;
+    for (int k = 0; k < K; ++k) scr[k * WAVE + lane] = scr[k * WAVE + lane] * rp;
+  };
   if (root) draws();
   if (!root) run_mlp<KM>(A, st, L, draws);
   if (st.role == VBN_ROLE_PARAMS) {
@@ -867,21 +891,7 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
   }
   if (!root) {
     min_scale = t[0];
-    // pi = softmax(logits).clamp_min(1e-5); pi /= sum (mdn.py:227-228)
-    lmax = -INFINITY;
-    for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, scr[k * WAVE + lane]);
-    lsum = 0.f;
-    for (int k = 0; k < K; ++k) lsum += __expf(scr[k * WAVE + lane] - lmax);
-    // pi_k computed once per particle into the logit rows (the inverse CDF and the log-prob
-    // read pi_k repeatedly; same operations, so the same values)
-    psum = 0.f;
-    for (int k = 0; k < K; ++k) {
-      const float p = fmaxf(__expf(scr[k * WAVE + lane] - lmax) / lsum, 1e-5f);
-      scr[k * WAVE + lane] = p;
-      psum += p;
-    }
-    psum = fmaxf(psum, 1e-12f);
-    for (int k = 0; k < K; ++k) scr[k * WAVE + lane] = scr[k * WAVE + lane] / psum;
+    make_pi();
   }
   auto pi_k = [&](int k) -> float { return root ? t[k] : scr[k * WAVE + lane]; };
   auto loc_kd = [&](int k, int d) -> float {
@@ -977,11 +987,14 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
       const float2 uu = d == 0 ? uu0 : draw_uniforms(A, st, d, L);
       if (!root && !(st.flags & VBN_F_LOGP)) {
         // the logits are not read again: the class probabilities replace them, computed once
-        // (the inverse CDF reads each twice; same operations, so the same values)
-        for (int c = 0; c < C; ++c) L.scr[(d * C + c) * WAVE + lane] = __expf(logit(c) - m) / se;
+        // (the inverse CDF reads each twice; same operations, so the same values); one
+        // reciprocal of the sum instead of C divisions
+        const float rse = 1.0f / se;
+        for (int c = 0; c < C; ++c) L.scr[(d * C + c) * WAVE + lane] = __expf(logit(c) - m) * rse;
         idx = inv_cdf(C, uu.x, [&](int c) { return L.scr[(d * C + c) * WAVE + lane]; });
       } else {
-        idx = inv_cdf(C, uu.x, [&](int c) { return __expf(logit(c) - m) / se; });
+        const float rse = 1.0f / se;
+        idx = inv_cdf(C, uu.x, [&](int c) { return __expf(logit(c) - m) * rse; });
       }
       const float left = e[idx];
       const float right = e[idx + 1 < C ? idx + 1 : C];
