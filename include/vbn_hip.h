@@ -100,6 +100,9 @@ enum vbn_role {
 #define VBN_F_MLP_GENERIC 2048  /* NN CPD with hidden_dims other than (32, 32): every layer as
                                    exact f32 MFMA tiles through LDS; off_w2 points at the layer
                                    table [L, (in, out, off_w, off_b) x L] (int32 in the blob)   */
+#define VBN_F_HEAD_MFMA 4096    /* NN CPD head (8..32 outputs) on the split-f16 MFMA like layer 2:
+                                   reserved[2] = its fragments [hi 2][64][8 f16] ++ [lo ...]
+                                   (1024 floats), then the accumulator-init bias [2][16]      */
 
 /* activations of the NN CPDs (reference gaussian_nn.py:19-24) */
 enum vbn_act { VBN_ACT_RELU = 0, VBN_ACT_TANH = 1, VBN_ACT_GELU = 2, VBN_ACT_ELU = 3 };
@@ -117,7 +120,8 @@ enum vbn_mode {
 };
 
 /* One node of the topological walk (32 x int32, filled by the host plan packer).
- * reserved[0] = split-f16 W2 fragments; [1..4] = KDE point packs; [5] = wblk_off, [6] =
+ * reserved[0] = split-f16 W2 fragments; [1..4] = KDE point packs (NN steps: [1] = the layer-1
+ * operand bound zlim as float bits, [2] = the VBN_F_HEAD_MFMA head fragments); [5] = wblk_off, [6] =
  * wblk_len: the NN CPD's weight block [W1 fragments | layer-1/2 accumulator-init biases |
  * split-f16 W2 | W3 | b3], rounded up to a multiple of 256 floats (params float offset,
  * length in floats), which the walk stages into LDS one step ahead (0 = the step runs no

@@ -493,6 +493,51 @@ __device__ __forceinline__ void head_outputs_n(const float* __restrict__ w3, con
   }
 }
 
+// Wide heads (VBN_F_HEAD_MFMA: mdn, softmax_nn; 8..32 outputs) on the split-f16 MFMA like
+// layer 2: the layer-2 activations are already in the B-operand layout, W3 is packed as layer
+// 2's A fragments (output rows padded to 32) and the bias is the accumulator init, so the head
+// is 6 MFMAs and one f16 split per group instead of 16 FMAs per output per group.  Lane half h
+// of group g then holds outputs row(r, h) of particle (lane & 31) + 32 g, stored to the head
+// rows.  Activations beyond the split range, or a NaN parent input, take the VALU head.
+__host__ __device__ constexpr bool head_on_mfma(int flags) {
+  return (flags & VBN_F_HEAD_MFMA) != 0 && (flags & VBN_F_F32L2) == 0;
+}
+
+template <int ACT, bool MIR>
+__device__ __forceinline__ void head_mfma(const vbn_step& st, const Lane& L, const float* __restrict__ W,
+                                          const f32x16& h0, const f32x16& h1, bool nan_in) {
+  const int lane = L.lane;
+  float y0[16], y1[16];
+  int big = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    y0[r] = act_fn<ACT>(h0[r]);
+    y1[r] = MIR ? y0[r] : act_fn<ACT>(h1[r]);
+    big = max(big, max(__float_as_int(y0[r]), __float_as_int(y1[r])));   // positive side only
+  }
+  if (__any(big > 0x47000000 || nan_in)) {         // rare: the VALU head
+    mlp_head<ACT>(st, L, W, h0, h1, nan_in);
+    return;
+  }
+  const float* __restrict__ F = L.P + st.reserved[2];
+  const uint4* w3h = reinterpret_cast<const uint4*>(F);
+  const uint4 wq[4] = {w3h[lane], w3h[WAVE + lane], w3h[2 * WAVE + lane], w3h[3 * WAVE + lane]};
+  const f32x16 bi = load_acc16(F + 1024 + 16 * (lane >> 5));
+  const f32x16 o0 = layer2_split(wq, bi, y0);
+  const f32x16 o1 = MIR ? o0 : layer2_split(wq, bi, y1);
+  const int h = lane >> 5, n = lane & 31;
+  float* __restrict__ scr = L.scr;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+    if (row < st.n_out) {
+      scr[row * WAVE + n] = o0[r];
+      scr[row * WAVE + n + 32] = o1[r];
+    }
+  }
+  wave_sync();
+}
+
 // One NN node for the wave's 64 particles from the LDS-staged weight block.  Group 0 (layer 1,
 // layer 2 split-f16 on MFMA), group 1, the head on both -- one basic block: the f16 range
 // check only ORs a wave-uniform flag, and the rare exact path (an activation beyond the split
@@ -537,6 +582,8 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
     head_outputs_n<NOUT>(W + (st.off_w3 - WBLK_OFF(st)) + 16 * (lane >> 5), W + (st.off_b3 - WBLK_OFF(st)),
                          L.scr + lane, y0, y1, nan_in);
     wave_sync();
+  } else if (head_on_mfma(st.flags)) {
+    head_mfma<ACT, MIR>(st, L, W, h0, h1, nan_in);
   } else {
     mlp_head<ACT>(st, L, W, h0, h1, nan_in);
   }

@@ -44,6 +44,8 @@ WBLK_CHUNK = 256          # floats per LDS-DMA wave instruction (64 lanes x 16 B
 KDE_CHUNKS = 16
 KDE_REC_TAIL = 8       # weight-0 record rows after the last point (csrc kde_scan prefetch)
 MLP_HIDDEN = (32, 32)
+HEAD_MFMA_MIN = 8         # heads at least this wide run on MFMA (csrc head_mfma)
+F_HEAD_MFMA = 4096
 MAX_NODES = 1 << 14
 MAX_NODE_DIMS = 1 << 8
 
@@ -217,6 +219,7 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     else:
         offs["zlim"] = float(np.float32(min(room / rs, 3.0e38))) if rs > 0 else 3.0e38
     j = np.arange(8)
+    j3 = j
     frag = np.zeros((2, 64, 8), np.float32)
     for s in range(2):
         for ln in range(64):
@@ -229,6 +232,23 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     # head: row j = W3[j][row(r, 0)] (r < 16) ++ W3[j][row(r, 1)] (lane half h reads 16 at 16 h)
     offs["w3"] = blob.add(np.concatenate([w3[:, _ROWS[0]], w3[:, _ROWS[1]]], axis=1))  # [n_out, 32]
     offs["b3"] = blob.add(b3)
+    n_out = w3.shape[0]
+    if HEAD_MFMA_MIN <= n_out <= 32 and np.abs(w3).max() <= 32768.0:
+        # wide heads (mdn, softmax_nn) on the split-f16 MFMA like layer 2 (csrc head_mfma):
+        # W3 padded to 32 output rows in the layer-2 fragment layout, then the bias as the
+        # accumulator init [half h][16] = b3[row(r, h)] (0 beyond n_out); outside the block
+        w3p = np.zeros((32, 32), np.float32)
+        w3p[:n_out] = w3
+        f3 = np.zeros((2, 64, 8), np.float32)
+        for s_ in range(2):
+            for ln in range(64):
+                f3[s_, ln] = w3p[ln & 31, 16 * s_ + 8 * (j3 >> 2) + 4 * (ln >> 5) + (j3 & 3)]
+        hi3 = f3.astype(np.float16)
+        lo3 = (f3 - hi3.astype(np.float32)).astype(np.float16)
+        b3p = np.zeros(32, np.float32)
+        b3p[:n_out] = b3
+        offs["w3h"] = blob.add(np.concatenate([hi3, lo3]).reshape(-1).view(np.float32))   # 1024 floats
+        blob.add(b3p[_ROWS])                                                               # [2, 16]
     blen = offs["b3"] + b3.size - offs["wblk"]
     offs["wblk_len"] = -(-blen // WBLK_CHUNK) * WBLK_CHUNK
     offs["w2"] = blob.add(w2f.reshape(4, 4, 64).transpose(0, 2, 1))            # [4, 64, 4] (exact f32)
@@ -560,6 +580,10 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         row[S_OFF_KQ] = npk.offs.get("kq", -1)
         if "zlim" in npk.offs:                   # NN steps: layer-1 operand bound (f32 bits)
             row[S_OFF_KQ] = np.float32(npk.offs["zlim"]).view(np.int32)
+        if "w3h" in npk.offs:                    # NN steps: split-f16 head fragments
+            row[S_OFF_KQY] = npk.offs["w3h"]
+            fl |= F_HEAD_MFMA
+            row[S_FLAGS] = fl
         row[S_OFF_KQY] = npk.offs.get("kqy", -1)
         row[S_OFF_KR] = npk.offs.get("kr", -1)
         row[S_OFF_KV] = npk.offs.get("kv", -1)
