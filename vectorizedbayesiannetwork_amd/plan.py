@@ -580,11 +580,11 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         row[S_OFF_KQ] = npk.offs.get("kq", -1)
         if "zlim" in npk.offs:                   # NN steps: layer-1 operand bound (f32 bits)
             row[S_OFF_KQ] = np.float32(npk.offs["zlim"]).view(np.int32)
+        row[S_OFF_KQY] = npk.offs.get("kqy", -1)
         if "w3h" in npk.offs:                    # NN steps: split-f16 head fragments
             row[S_OFF_KQY] = npk.offs["w3h"]
             fl |= F_HEAD_MFMA
             row[S_FLAGS] = fl
-        row[S_OFF_KQY] = npk.offs.get("kqy", -1)
         row[S_OFF_KR] = npk.offs.get("kr", -1)
         row[S_OFF_KV] = npk.offs.get("kv", -1)
         row[S_OFF_KQ32] = npk.offs.get("kq32", -1)
