@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--cpu-chains", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wave-particles", type=int, default=None, help="32 / 64 (default: the engine's choice)")
+    ap.add_argument("--chain-waves", type=int, default=None,
+                    help="0..4: waves per chain workgroup of the specialised sweep (default: the engine's choice)")
     ap.add_argument("--plan-jit", choices=("auto", "on", "off"), default="auto",
                     help="plan-specialised sweep kernel (vectorizedbayesiannetwork_amd/jit.py) or the interpreter")
     args = ap.parse_args()
@@ -68,7 +70,7 @@ def main():
     query = {"target": query["target"],
              "evidence": {k: v.repeat(reps_ev, 1)[:B].contiguous() for k, v in query["evidence"].items()}}
     vbn.set_sampling_method("gibbs", n_samples=args.n_samples, burn_in=args.burn_in, n_steps=args.thin, seed=1,
-                            wave_particles=args.wave_particles, plan_jit=pj)
+                            wave_particles=args.wave_particles, plan_jit=pj, chain_waves=args.chain_waves)
     for _ in range(args.warmup):
         vbn.sample(query, n_samples=args.n_samples)
     torch.cuda.synchronize()
@@ -94,9 +96,11 @@ def main():
     def launch(seed):
         return ops.gibbs_walk(gp.steps, gp.in_cols, pk.params, fx, None, state, B, gp.init.n_slots,
                               gp.init.max_out, gp.init.fixed_ld, B, gp.n_noise, pk.dmax, 1, iters, iters - 1, 1,
-                              0, seed, 1, gp.kind_mask, gp.wbuf, wp, eng.plan_jit)
+                              0, seed, 1, gp.kind_mask, gp.wbuf, wp, eng.plan_jit,
+                              -1 if eng.chain_waves is None else eng.chain_waves)
     launch(0)
     specialised = bool(ops.LAST_WALK.get("specialised"))
+    chain_waves = int(ops.LAST_WALK.get("chain_waves") or 0)
     stream = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 3
@@ -120,7 +124,7 @@ def main():
         "data": "synthetic (cfg2 DAG/SEM/query generator; random-init CPD weights)",
         "config": {"workload": "gibbs32: 32node-gaussian_nn-gibbs", "chains": B, "n_samples": args.n_samples,
                    "burn_in": args.burn_in, "n_steps": args.thin, "sweeps": iters, "candidates": 8,
-                   "wave_particles": wp,
+                   "wave_particles": wp, "chain_waves": chain_waves,
                    "walk": "plan-specialised" if specialised else "step-table interpreter"},
         "roofline": {"bound": "mfma", "achieved": round(ach, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
                      "frac": round(ach / peak, 4), "traffic": None, "kernel": ("vbn_walk_plan" if specialised else "vbn_walk_kernel") + " (GIBBS)",

@@ -68,3 +68,76 @@ def test_reference_gibbs_collects_final_state():
         for case in load_golden(name)["cases"]:
             s = case["outputs"]["samples"]
             assert torch.equal(s, s[:, :1].expand_as(s))
+
+
+def _group_rw(rows, ic, b, e):
+    cols = lambda r: set(range(int(r[P.S_OUTCOL]), int(r[P.S_OUTCOL]) + int(r[P.S_OUTDIM])))
+    rd, wr = set(), cols(rows[b])
+    for k in range(b, e):
+        r = rows[k]
+        rd |= set(int(c) for c in ic[int(r[P.S_INOFF]):int(r[P.S_INOFF]) + int(r[P.S_NIN])])
+        if int(r[P.S_ROLE]) == P.ROLE_FIXED:
+            rd |= cols(r)
+    return rd, wr
+
+
+@pytest.mark.parametrize("name", NAMES + ["cfg2"])
+@pytest.mark.parametrize("n_waves", [1, 2, 4])
+def test_gibbs_levels_schedule(name, n_waves):
+    """plan.gibbs_levels: every node update (LATENT .. SELECT) runs exactly once per sweep, the
+    updates of one level touch no slot another one writes, and every conflicting pair keeps its
+    sweep order -- so the wave-parallel sweep is the sequential one, bit for bit."""
+    if name == "cfg2":
+        import bench
+        cfg, model, target, ev = bench.build_model("cfg2")
+        cases = [{"query": {"target": target, "evidence": dict.fromkeys(ev), "do": {}}}]
+    else:
+        fx = load_golden(name)
+        model = model_from_checkpoint(fx["model"])
+        cases = fx["cases"]
+    pk = P.PackedModel(model, torch.device("cpu"))
+    for case in cases:
+        q = case["query"]
+        fixed = set(q["evidence"]) | set(q["do"])
+        gp = P.build_gibbs_plan(pk, latent=[n for n in model.topo if n not in fixed],
+                                fixed=[n for n in model.topo if n in fixed], target=q["target"])
+        rows, ic, _ = gp.steps._vbn_host
+        levels = P.gibbs_levels(rows, ic, n_waves)
+        assert all(len(lv) == n_waves for lv in levels)
+        ranges = [(lv, w, b, e) for lv, waves in enumerate(levels) for w, rs in enumerate(waves) for b, e in rs]
+        covered = sorted(i for _, _, b, e in ranges for i in range(b, e))
+        assert covered == list(range(len(rows)))                        # each step exactly once
+        coll = [r for r in ranges if rows[r[2]][P.S_ROLE] == P.ROLE_COLLECT]
+        assert coll and all(lv == len(levels) - 1 and w == 0 for lv, w, _, _ in coll)
+        groups = [r for r in ranges if rows[r[2]][P.S_ROLE] == P.ROLE_LATENT]
+        assert len(groups) == len(gp.latent)
+        for i, (lv1, _, b1, e1) in enumerate(groups):
+            r1, w1 = _group_rw(rows, ic, b1, e1)
+            for lv2, _, b2, e2 in groups[i + 1:]:
+                r2, w2 = _group_rw(rows, ic, b2, e2)
+                conflict = bool(w1 & (r2 | w2) or r1 & w2)
+                if lv1 == lv2:
+                    assert not conflict
+                if conflict:
+                    assert (lv1 < lv2) == (b1 < b2)
+        if len(groups) > 2 and n_waves > 1:
+            assert len(levels) < len(groups) + 1                         # some updates run together
+
+
+def test_chain_sweep_source():
+    """jit.plan_source with a level schedule: the chain-workgroup sweep, every step once."""
+    import bench
+    from vectorizedbayesiannetwork_amd import jit
+    cfg, model, target, ev = bench.build_model("cfg2")
+    pk = P.PackedModel(model, torch.device("cpu"))
+    gp = P.build_gibbs_plan(pk, latent=[n for n in model.topo if n not in ev],
+                            fixed=[n for n in model.topo if n in ev], target=target)
+    rows, ic, _ = gp.steps._vbn_host
+    levels = P.gibbs_levels(rows, ic, 4)
+    src = jit.plan_source(rows, ic, gp.kind_mask | 64 | 256, levels)
+    assert "#define VBN_PLAN_CHAIN_WAVES 4" in src
+    assert src.count("__syncthreads();") == len(levels)
+    import re
+    idx = [int(x) for seq in re.findall(r"vbn_seq<int, ([0-9, ]+)>", src) for x in seq.split(",")]
+    assert sorted(idx) == list(range(len(rows)))
+    assert "VBN_PLAN_CHAIN_WAVES" not in jit.plan_source(rows, ic, gp.kind_mask | 64 | 256)

@@ -85,3 +85,60 @@ def test_specialised_gibbs_sweeps_bit_identical(wave_particles):
     assert not s0 and s1, f"specialisation flags {s0}, {s1} ({jit._failed})"
     assert got.shape == ref.shape and torch.isfinite(ref).all()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("wave_particles", [32, 64])
+@pytest.mark.parametrize("chain_waves", [1, 2, 4])
+def test_chain_workgroup_gibbs_bit_identical(wave_particles, chain_waves):
+    """Gibbs sweeps on chain workgroups (plan.gibbs_levels: the waves of a workgroup split each
+    sweep's node updates by level): the chains equal the sequential interpreter's bit for bit,
+    production draws, several collected sweeps, chains that do not fill the last workgroup."""
+    from vectorizedbayesiannetwork_amd import jit, ops
+    from vectorizedbayesiannetwork_amd.engines import GibbsSampler, Query
+    if not jit.enabled():
+        pytest.skip("VBN_PLAN_JIT=0")
+    model, vbn, target, ev = synthetic_workload("cfg2", 13, "cuda")
+    q = Query(target, {k: v.cuda() for k, v in ev.items()})
+    outs = []
+    for pj, cw in ((False, 0), (True, chain_waves)):
+        eng = GibbsSampler(n_samples=6, burn_in=3, n_steps=2, collect="chain", wave_particles=wave_particles,
+                           plan_jit=pj, chain_waves=cw)
+        xs = eng.sample(vbn, q, 6, seed=77)
+        torch.cuda.synchronize()
+        outs.append((xs.clone(), bool(ops.LAST_WALK.get("specialised")), ops.LAST_WALK.get("chain_waves")))
+    (ref, s0, _), (got, s1, c1) = outs
+    assert not s0 and s1 and c1 == chain_waves, f"flags {s0}, {s1}, {c1} ({jit._failed})"
+    assert got.shape == ref.shape and torch.isfinite(ref).all()
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("name", ["ext_gibbs_mix10", "ext_gibbs_kde6"])
+def test_chain_workgroup_gibbs_against_oracle(name):
+    """Chain-workgroup sweeps with the reference's recorded draws injected (every CPD family of
+    the fixtures: mixed kinds, KDE): the collected chains match the oracle and the reference's
+    own outputs, and equal the sequential interpreter bit for bit."""
+    from conftest import load_golden
+    from golden_noise import gibbs_noise
+    from oracle import vbn_oracle as O
+    from vectorizedbayesiannetwork_amd import VBN, jit, ops
+    from vectorizedbayesiannetwork_amd.engines import GibbsSampler
+    from vectorizedbayesiannetwork_amd.model import model_from_checkpoint
+    if not jit.enabled():
+        pytest.skip("VBN_PLAN_JIT=0")
+    fx = load_golden(name)
+    model = model_from_checkpoint(fx["model"])
+    vbn = VBN.from_model(model, device="cuda:0")
+    for case in fx["cases"][:2]:
+        q, n, p = case["query"], case["n_samples"], case["params"]
+        qq = vbn._normalize_query(q)
+        latent = [x for x in model.topo if x not in q["evidence"] and x not in q["do"]]
+        noise = gibbs_noise(case, model, latent, max(model.out_dim(x) for x in model.topo))
+        ref = GibbsSampler(n_samples=n, collect="chain", plan_jit=False, **p).sample(vbn, qq, n, _noise=noise)
+        e = GibbsSampler(n_samples=n, collect="chain", plan_jit=True, chain_waves=4, **p)
+        got = e.sample(vbn, qq, n, _noise=noise)
+        torch.cuda.synchronize()
+        assert ops.LAST_WALK.get("chain_waves") == 4, jit._failed
+        assert torch.equal(torch.nan_to_num(got, 7.0), torch.nan_to_num(ref, 7.0))
+        rxc = O.gibbs(model, q["target"], q["evidence"], q["do"], n, O.ReplayDraws(case["draws"]),
+                      copy_collected=True, **p)
+        assert torch.allclose(got.cpu(), rxc, rtol=1e-4, atol=1e-4, equal_nan=True)

@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -29,6 +29,7 @@ EXPORTS = (
     "vbn_hip_module_load",
     "vbn_hip_walk_module",
     "vbn_hip_module_unload",
+    "vbn_hip_module_chain_waves",
 )
 
 
@@ -128,6 +129,8 @@ def load(path: str = None) -> ctypes.CDLL:
         lib.vbn_hip_walk_module.restype = ctypes.c_int
         lib.vbn_hip_module_unload.argtypes = [ctypes.c_void_p]
         lib.vbn_hip_module_unload.restype = ctypes.c_int
+        lib.vbn_hip_module_chain_waves.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        lib.vbn_hip_module_chain_waves.restype = ctypes.c_int
         lib.vbn_hip_struct_size.argtypes = [ctypes.c_int]
         lib.vbn_hip_struct_size.restype = ctypes.c_int
         if lib.vbn_hip_struct_size(0) != ctypes.sizeof(VbnWalkArgs) or lib.vbn_hip_struct_size(1) != 128:

@@ -2,6 +2,7 @@
 // (weight normalisation, RB epilogue, resampling, posterior statistics).  The walk kernel
 // lives in vbn_walk_impl.h; its kind-set instantiations are compiled one per object from
 // walk_inst.hip and launched through vbn_launch_walk_km<KM>.
+#include "vbn_hip.h"
 #include "vbn_walk_impl.h"
 
 // the walk launchers, one per object compiled from walk_inst.hip
@@ -428,6 +429,7 @@ struct vbn_plan_module {
   hipFunction_t fn;
   unsigned kmi;
   int n_steps;
+  int chain_waves;     // > 0: a Gibbs sweep on chain workgroups (vbn_hip_module_chain_waves)
 };
 
 extern "C" int vbn_hip_module_load(const void* image, const char* kernel, uint32_t kind_set, int32_t n_steps,
@@ -455,6 +457,14 @@ extern "C" int vbn_hip_module_unload(void* handle) {
   return e == hipSuccess ? 0 : fail((int)e, hipGetErrorString(e));
 }
 
+extern "C" int vbn_hip_module_chain_waves(void* handle, int32_t n_waves) {
+  vbn_plan_module* m = (vbn_plan_module*)handle;
+  if (!m || n_waves < 1 || n_waves > WG_MAX_WAVES)
+    return fail(VBN_E_ARGS, "vbn_hip_module_chain_waves: bad module or wave count (1..4)");
+  m->chain_waves = n_waves;
+  return 0;
+}
+
 extern "C" int vbn_hip_walk_module(const void* handle, const vbn_walk_args* a, void* stream) {
   const vbn_plan_module* m = (const vbn_plan_module*)handle;
   if (!m) return fail(VBN_E_ARGS, "vbn_hip_walk_module: no module");
@@ -463,6 +473,21 @@ extern "C" int vbn_hip_walk_module(const void* handle, const vbn_walk_args* a, v
   if (rc) return rc;
   if (w.kmi != m->kmi || a->n_steps != m->n_steps)
     return fail(VBN_E_ARGS, "vbn_hip_walk_module: the launch does not match the compiled plan (kind set / steps)");
+  if (m->chain_waves > 0) {
+    // chain workgroups: every wave of a workgroup walks the same wp candidate lanes; one LDS
+    // copy of their slots + per-wave scratch rows, no weight buffers
+    if (a->mode != VBN_MODE_GIBBS)
+      return fail(VBN_E_ARGS, "vbn_hip_walk_module: a chain-workgroup module runs Gibbs sweeps only");
+    const int64_t wp = a->wave_particles == 32 ? 32 : WAVE;
+    const int64_t rows = a->max_out > 0 ? a->max_out : 1;
+    const int64_t lds = ((int64_t)a->n_slots + m->chain_waves * rows) * WAVE * (int64_t)sizeof(float);
+    if (lds > 160 * 1024) return fail(VBN_E_LDS, "vbn_hip_walk_module: chain workgroup needs more than 160 KiB of LDS");
+    const int64_t blocks = (a->n_queries * (int64_t)a->n_samples + wp - 1) / wp;
+    if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
+    w.grid = dim3((unsigned)blocks);
+    w.block = dim3(WAVE * m->chain_waves);
+    w.lds = (size_t)lds;
+  }
   vbn_walk_args args = *a;
   const float* params = a->params;
   void* kp[] = {&args, &params};

@@ -34,7 +34,7 @@
 #include <algorithm>
 #endif
 
-#include "vbn_hip.h"
+#include "vbn_hip_types.h"
 
 #ifndef INFINITY
 #define INFINITY __builtin_inff()
@@ -500,7 +500,11 @@ __device__ __forceinline__ void head_outputs_n(const float* __restrict__ w3, con
 // of group g then holds outputs row(r, h) of particle (lane & 31) + 32 g, stored to the head
 // rows.  Activations beyond the split range, or a NaN parent input, take the VALU head.
 __host__ __device__ constexpr bool head_on_mfma(int flags) {
+#ifdef VBN_ABL_NOHEADMFMA      // A/B only: every head on VALU (outputs within an ulp, not bitwise)
+  return false;
+#else
   return (flags & VBN_F_HEAD_MFMA) != 0 && (flags & VBN_F_F32L2) == 0;
+#endif
 }
 
 template <int ACT, bool MIR>

@@ -175,6 +175,84 @@ __device__ __forceinline__ void vbn_walk_plan_general(const vbn_walk_args& A, co
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Gibbs sweeps on chain workgroups (VBN_PLAN_CHAIN_WAVES waves per workgroup, jit.py with a
+// plan.gibbs_levels schedule).  A sweep at a few thousand chains leaves ~1 wave per SIMD, and
+// that wave's serial path (83 dependent steps for the cfg2 DAG) is the bound, not issue.  Here
+// the waves of a workgroup share ONE copy of their chains' slots in LDS and split each sweep's
+// node updates between them: the updates of one level touch no slot another one writes, so
+// they run at the same time on different waves, with one barrier per level (cfg2 DAG: 31
+// serial steps instead of 83 on 4 waves).  Every update runs the same device functions on the
+// same values with the same draws (keyed by node, chain and sweep) as in the sequential sweep,
+// so the chains are bit-identical to it.  Weights come from the blob (L1/L2): the waves run
+// different MLPs at once, so there is no per-workgroup staging.
+#ifdef VBN_PLAN_CHAIN_WAVES
+template <unsigned KM, int I>
+__device__ __forceinline__ void vbn_plan_step_direct(const vbn_walk_args& A, const float* __restrict__ params,
+                                                     Lane& L, float& lp) {
+  constexpr vbn_step st = VBN_PLAN_STEPS[I];
+  L.wb = params + st.reserved[5];
+  walk_step<KM>(A, st, L, lp);
+}
+
+template <unsigned KM, int... I>
+__device__ __forceinline__ void vbn_plan_run(const vbn_walk_args& A, const float* __restrict__ params, Lane& L,
+                                             float& lp, vbn_seq<int, I...>) {
+  (vbn_plan_step_direct<KM, I>(A, params, L, lp), ...);
+}
+
+// defined by the including unit (jit.py): every level's step ranges per wave, a barrier after each
+template <unsigned KM>
+__device__ __forceinline__ void vbn_plan_sweep_levels(const vbn_walk_args& A, const float* __restrict__ params,
+                                                      int wave, Lane& L, float& lp);
+
+template <unsigned KM>
+__device__ __forceinline__ void vbn_walk_plan_chains(const vbn_walk_args& A, const float* __restrict__ params) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rows = A.max_out > 0 ? A.max_out : 1;
+  Lane L;
+  L.P = params;
+  L.ic = VBN_PLAN_IC;
+  L.lane = threadIdx.x & (WAVE - 1);
+  L.vals = smem;                                       // the workgroup's chains, one copy
+  L.scr = smem + A.n_slots * WAVE + wave * rows * WAVE;   // per-wave head / scratch rows
+  L.wb = params;
+  const int64_t total = A.n_queries * (int64_t)A.n_samples;
+  L.mirror = (KM & 64) != 0;
+  L.lean = false;
+  L.noiseless = (KM & 256) != 0;
+  L.bm_spare = 0.f;
+  L.wq = false;
+  const int wp = L.mirror ? 32 : WAVE;
+  const int64_t p_raw = (int64_t)blockIdx.x * wp + (L.lane & (wp - 1));   // every wave: the same chains
+  const bool valid = p_raw < total;
+  L.p = valid ? p_raw : total - 1;
+  L.b = L.p / A.n_samples;
+  L.s = (int)(L.p - L.b * A.n_samples);
+  L.iter = 0;
+  L.valid = valid && wave == 0;                        // COLLECT: wave 0 writes the chains' outputs
+  float lp = 0.f;
+  if (A.state && (A.state_flags & 1)) {                // the start state (one ancestral pass)
+    if (wave == 0)
+      for (int c = 0; c < A.n_slots; ++c) vwrite(L, c, A.state[(int64_t)c * total + L.p]);
+    lp = A.state[(int64_t)A.n_slots * total + L.p];
+    __syncthreads();
+  }
+  for (int it = 0; it < A.gibbs_iters; ++it) {
+    L.iter = it;
+    const float* P = params;
+    const int32_t* IC = VBN_PLAN_IC;
+    vbn_walk_args S = A;
+    asm volatile("" : "+s"(P), "+s"(IC), "+s"(S.fixed), "+s"(S.noise), "+s"(S.seed), "+s"(S.offset),
+                 "+s"(S.q_base), "+s"(S.out_x));
+    L.P = P;
+    L.ic = IC;
+    vbn_plan_sweep_levels<KM>(S, P, wave, L, lp);
+  }
+}
+#endif
+
 template <unsigned KM>
 __device__ __forceinline__ void vbn_walk_plan_body(const vbn_walk_args& A, const float* __restrict__ params) {
   if constexpr ((KM & 128u) != 0) {      // lean (production MCM / IS / LW / ancestral): one pass
@@ -214,6 +292,10 @@ __device__ __forceinline__ void vbn_walk_plan_body(const vbn_walk_args& A, const
       for (int k = 0; k < A.n_out_cols; ++k) A.out_x[L.p * A.n_out_cols + k] = vread(L, A.out_cols[k]);
     }
   } else {
+#ifdef VBN_PLAN_CHAIN_WAVES
+    vbn_walk_plan_chains<KM>(A, params);
+#else
     vbn_walk_plan_general<KM>(A, params);
+#endif
   }
 }

@@ -590,11 +590,14 @@ class GibbsSampler(_EngineBase):
     HALF_WAVE_BELOW = 1536 * 64
 
     def __init__(self, n_samples: int = 200, burn_in: int = 10, n_steps: int = 1, collect: str = "reference",
-                 wave_particles: Optional[int] = None, **kwargs):
+                 wave_particles: Optional[int] = None, chain_waves: Optional[int] = None, **kwargs):
         super().__init__(n_samples=n_samples, **kwargs)
         if wave_particles not in (None, 32, 64):
             raise ValueError(f"wave_particles must be None (auto), 32 or 64, got {wave_particles!r}")
+        if chain_waves not in (None, 0, 1, 2, 3, 4):
+            raise ValueError(f"chain_waves must be None (auto) or 0..4, got {chain_waves!r}")
         self.wave_particles = wave_particles
+        self.chain_waves = chain_waves    # specialised sweeps: waves splitting a chain group's updates
         self.burn_in = int(burn_in)
         self.n_steps = int(n_steps)
         self.n_candidates = 8
@@ -661,7 +664,8 @@ class GibbsSampler(_EngineBase):
         out = ops.gibbs_walk(gp.steps, gp.in_cols, pk.params, fx,
                              sweep_noise, chains.contiguous(), b, init.n_slots, init.max_out, init.fixed_ld,
                              noise_b, gp.n_noise, pk.dmax, dt, iters, burn, th, self.q_base, seed, 1,
-                             gp.kind_mask, gp.wbuf, self._wave_particles(b), self.plan_jit)
+                             gp.kind_mask, gp.wbuf, self._wave_particles(b), self.plan_jit,
+                             -1 if self.chain_waves is None else self.chain_waves)
         if self.collect == "chain" and n > 0:
             return out
         return out.expand(b, max(n, 1), dt).contiguous()

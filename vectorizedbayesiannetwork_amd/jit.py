@@ -50,22 +50,45 @@ def enabled() -> bool:
     return os.environ.get("VBN_PLAN_JIT", "1") != "0"
 
 
-def plan_source(steps: np.ndarray, in_cols: np.ndarray, kind_set: int) -> str:
-    """The translation unit of one plan-specialised walk (csrc/vbn_walk_plan.h)."""
+def plan_source(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=None) -> str:
+    """The translation unit of one plan-specialised walk (csrc/vbn_walk_plan.h).  ``levels``
+    (plan.gibbs_levels: per level, per wave, step ranges) makes it a Gibbs sweep on chain
+    workgroups of ``len(levels[0])`` waves."""
     rows = []
     for r in np.asarray(steps, np.int32).reshape(-1, 32):
         v = [int(x) for x in r]
         rows.append("  {" + ", ".join(map(str, v[:24])) + ", {" + ", ".join(map(str, v[24:])) + "}},")
     ic = [int(x) for x in np.asarray(in_cols, np.int32).reshape(-1)] or [0]
+    chain, sweep = [], []
+    if levels:
+        chain = [f"#define VBN_PLAN_CHAIN_WAVES {len(levels[0])}"]
+        sweep = ["template <unsigned KM>",
+                 "__device__ __forceinline__ void vbn_plan_sweep_levels(const vbn_walk_args& A, "
+                 "const float* __restrict__ params, int wave, Lane& L, float& lp) {"]
+        for lv, waves in enumerate(levels):
+            sweep.append(f"  // level {lv}")
+            first = True
+            for w, ranges in enumerate(waves):
+                idx = [i for b, e in ranges for i in range(b, e)]
+                if not idx:
+                    continue
+                seq = ", ".join(map(str, idx))
+                sweep.append(f"  {'if' if first else 'else if'} (wave == {w}) "
+                             f"vbn_plan_run<KM>(A, params, L, lp, vbn_seq<int, {seq}>{{}});")
+                first = False
+            sweep.append("  __syncthreads();")
+        sweep.append("}")
     return "\n".join([
         "// plan-specialised walk (vectorizedbayesiannetwork_amd/jit.py)",
         '#include "vbn_walk_impl.h"',
         f"#define VBN_PLAN_N_STEPS {len(rows)}",
+        *chain,
         "constexpr vbn_step VBN_PLAN_STEPS[VBN_PLAN_N_STEPS] = {",
         *rows,
         "};",
         f"__constant__ int32_t VBN_PLAN_IC[{len(ic)}] = {{{', '.join(map(str, ic))}}};",
         '#include "vbn_walk_plan.h"',
+        *sweep,
         f'extern "C" __global__ void __launch_bounds__(WG_MAX_WAVES * WAVE) '
         f"__attribute__((amdgpu_waves_per_eu(VBN_WPE))) {KERNEL}(const vbn_walk_args A, "
         f"const float* __restrict__ params) {{ vbn_walk_plan_body<{int(kind_set)}u>(A, params); }}",
@@ -134,15 +157,15 @@ def _version_tag() -> str:
 def _headers_digest() -> str:
     h = hashlib.sha256()
     for p in (os.path.join(CSRC, "vbn_walk_impl.h"), os.path.join(CSRC, "vbn_walk_plan.h"),
-              os.path.join(INCLUDE, "vbn_hip.h")):
+              os.path.join(INCLUDE, "vbn_hip.h"), os.path.join(INCLUDE, "vbn_hip_types.h")):
         with open(p, "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
 
 
-def code_object(steps: np.ndarray, in_cols: np.ndarray, kind_set: int) -> Tuple[str, bytes]:
+def code_object(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=None) -> Tuple[str, bytes]:
     """(cache key, code object) of a plan, from the disk cache or compiled."""
-    src = plan_source(steps, in_cols, kind_set)
+    src = plan_source(steps, in_cols, kind_set, levels)
     key = hashlib.sha256("\n".join([src, " ".join(OPTIONS), _version_tag(), _headers_digest()]).encode()
                          ).hexdigest()[:32]
     d = _cache_dir()
@@ -164,11 +187,12 @@ def code_object(steps: np.ndarray, in_cols: np.ndarray, kind_set: int) -> Tuple[
 
 
 def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_index: int,
-               plan_key: str) -> Optional[int]:
+               plan_key: str, chain_waves: int = 0) -> Optional[int]:
     """Loaded module handle for (plan, kind set, device), compiling on first use; None if the
-    plan cannot be specialised here (the caller runs the interpreter)."""
+    plan cannot be specialised here (the caller runs the interpreter).  ``chain_waves`` > 0:
+    a Gibbs sweep table run on chain workgroups of that many waves (plan.gibbs_levels)."""
     global _warned
-    mk = (device_index, f"{plan_key}:{kind_set}")
+    mk = (device_index, f"{plan_key}:{kind_set}:{chain_waves}")
     h = _modules.get(mk)
     if h is not None:
         return h
@@ -179,12 +203,18 @@ def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_ind
         if mk[1] in _failed:
             return None
         try:
-            _, code = code_object(steps, in_cols, kind_set)
+            levels = None
+            if chain_waves > 0:
+                from .plan import gibbs_levels
+                levels = gibbs_levels(steps, in_cols, chain_waves)
+            _, code = code_object(steps, in_cols, kind_set, levels)
             lib = _lib.load()
             handle = ctypes.c_void_p()
             buf = ctypes.create_string_buffer(code, len(code))
             _lib.check(lib.vbn_hip_module_load(buf, KERNEL.encode(), kind_set, len(steps), ctypes.byref(handle)),
                        "vbn_hip_module_load")
+            if chain_waves > 0:
+                _lib.check(lib.vbn_hip_module_chain_waves(handle, chain_waves), "vbn_hip_module_chain_waves")
             _modules[mk] = handle.value
             STATS["loaded"] += 1
             return handle.value

@@ -167,10 +167,11 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
 LAST_WALK = {"specialised": False}
 
 
-def _plan_module(lib, a, steps, step_begin, step_end, work, plan_jit, device):
+def _plan_module(lib, a, steps, step_begin, step_end, work, plan_jit, device, chain_waves=0):
     """Module handle of the plan-specialised walk for this launch, or None (interpreter).
     ``work`` = particles x sweeps; ``plan_jit`` 1 (auto: launches without injected draws of at
-    least jit.JIT_MIN_PARTICLES particle-steps) or 2 (always)."""
+    least jit.JIT_MIN_PARTICLES particle-steps) or 2 (always); ``chain_waves`` > 0: a Gibbs sweep
+    on chain workgroups of that many waves (:func:`gibbs_walk`)."""
     if not plan_jit or step_begin != 0 or step_end != steps.shape[0]:
         return None
     from . import jit
@@ -182,7 +183,8 @@ def _plan_module(lib, a, steps, step_begin, step_end, work, plan_jit, device):
     km = lib.vbn_hip_walk_kind_set(ctypes.byref(a))
     if km <= 0:
         return None
-    return jit.module_for(host[0], host[1], km, device.index if device.index is not None else 0, host[2])
+    return jit.module_for(host[0], host[1], km, device.index if device.index is not None else 0, host[2],
+                          chain_waves)
 
 
 @walk.register_fake
@@ -200,13 +202,19 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
                state: Tensor, n_queries: int, n_slots: int, max_out: int, fixed_ld: int, noise_b: int,
                n_noise: int, dmax: int, out_dim: int, iters: int, burn_in: int, thin: int, q_base: int,
                seed: int, offset: int, kind_mask: int, wbuf: int = 0, wave_particles: int = 64,
-               plan_jit: int = 1) -> Tensor:
+               plan_jit: int = 1, chain_waves: int = -1) -> Tensor:
     """``iters`` Gibbs sweeps (gibbs.py:34-87) over B chains x 8 candidate lanes, started from
     ``state`` [n_slots + 1, B*8]; returns the collected target values [B, n_collect, out_dim].
     ``wave_particles`` 32: half-wave launch (4 chains per wave64, include/vbn_hip.h).
-    ``plan_jit`` as for :func:`walk` (0 interpreter, 1 auto, 2 always specialised)."""
+    ``plan_jit`` as for :func:`walk` (0 interpreter, 1 auto, 2 always specialised).
+    ``chain_waves`` (specialised sweeps only): 1..4 = chain workgroups of that many waves that
+    split each sweep's node updates by level (plan.gibbs_levels; bit-identical chains), 0 = one
+    wave per chain group, -1 = auto (chain workgroups of 4 when the one-wave form would leave
+    fewer than 2 waves per SIMD, CHAIN_WAVES_BELOW)."""
     if wave_particles not in (32, 64):
         raise ValueError(f"vbn_hip::gibbs_walk: wave_particles must be 32 or 64, got {wave_particles}")
+    if not -1 <= chain_waves <= 4:
+        raise ValueError(f"vbn_hip::gibbs_walk: chain_waves must be -1 (auto) or 0..4, got {chain_waves}")
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::gibbs_walk runs on the GPU only (no CPU fallback); "
@@ -267,19 +275,28 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
     lib = _lib.load()
     with torch.cuda.device(device):
         stream = ctypes.c_void_p(_stream_handle(device))
-        module = _plan_module(lib, a, steps, 0, int(steps.shape[0]), total * iters, plan_jit, device)
+        cw = chain_waves
+        if cw < 0:
+            cw = 4 if total // wave_particles < CHAIN_WAVES_BELOW else 0
+        module = _plan_module(lib, a, steps, 0, int(steps.shape[0]), total * iters, plan_jit, device, cw)
         if module is not None:
             _lib.check(lib.vbn_hip_walk_module(ctypes.c_void_p(module), ctypes.byref(a), stream), "vbn_hip_walk_module")
         else:
             _lib.check(lib.vbn_hip_walk(ctypes.byref(a), stream), "vbn_hip_walk")
     LAST_WALK["specialised"] = module is not None
+    LAST_WALK["chain_waves"] = cw if module is not None else 0
     return x
+
+
+# Gibbs launches whose one-wave form has fewer waves than this (2 per SIMD on 1024 SIMDs) run
+# the specialised sweep on chain workgroups of 4 waves
+CHAIN_WAVES_BELOW = 2048
 
 
 @gibbs_walk.register_fake
 def _gibbs_walk_fake(steps, in_cols, params, fixed, noise, state, n_queries, n_slots, max_out, fixed_ld,
                      noise_b, n_noise, dmax, out_dim, iters, burn_in, thin, q_base, seed, offset, kind_mask, wbuf=0,
-                     wave_particles=64, plan_jit=1):
+                     wave_particles=64, plan_jit=1, chain_waves=-1):
     return params.new_empty((n_queries, (iters - burn_in + thin - 1) // thin, out_dim))
 
 

@@ -721,3 +721,77 @@ def build_gibbs_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Seque
     return GibbsPlan(init=init, steps=steps, n_steps=len(table), latent=lat, target=target,
                      n_noise=max(2 * len(lat), 1), in_cols=full.in_cols, kind_mask=full.kind_mask,
                      wbuf=int(tab[:, S_WBLK_LEN].max()))
+
+
+def gibbs_levels(tab: np.ndarray, in_cols: np.ndarray, n_waves: int) -> List[List[List[Tuple[int, int]]]]:
+    """Wave-parallel schedule of one Gibbs sweep table (csrc vbn_walk_plan.h, chain workgroups).
+
+    A node update -- its LATENT step, one FIXED + KEEP step per child, its SELECT step -- reads
+    the slots of its Markov blanket (parents, children, the children's other parents) and
+    writes its own.  Two updates that touch no slot the other writes commute, so running them
+    at the same time on different waves gives bit-for-bit the sequential sweep (same draws,
+    which are keyed by node and sweep, and the same operations on the same values).  Level of
+    an update = 1 + the highest level of an earlier update it conflicts with; the updates of a
+    level are spread over ``n_waves`` waves (longest first, by step count), and the COLLECT
+    steps form a last level on wave 0.
+
+    Returns ``levels[l][w]`` = the (begin, end) step ranges wave w runs in level l, in sweep
+    order.  A child's FIXED + KEEP step writes back the value it read (the same bits), which is
+    a read for this analysis.
+    """
+    n = len(tab)
+    groups: List[Tuple[int, int]] = []
+    collect: List[int] = []
+    i = 0
+    while i < n:
+        role = int(tab[i, S_ROLE])
+        if role == ROLE_COLLECT:
+            collect.append(i)
+            i += 1
+            continue
+        if role != ROLE_LATENT:
+            raise ValueError(f"gibbs_levels: step {i} (role {role}) outside a LATENT .. SELECT group")
+        j = i + 1
+        while j < n and int(tab[j, S_ROLE]) != ROLE_SELECT:
+            if int(tab[j, S_ROLE]) != ROLE_FIXED or not int(tab[j, S_FLAGS]) & F_KEEP:
+                raise ValueError(f"gibbs_levels: step {j} is not a child log-prob step")
+            j += 1
+        if j == n:
+            raise ValueError("gibbs_levels: LATENT step without its SELECT")
+        groups.append((i, j + 1))
+        i = j + 1
+
+    def cols(r):
+        return set(range(int(r[S_OUTCOL]), int(r[S_OUTCOL]) + int(r[S_OUTDIM])))
+
+    reads, writes = [], []
+    for b, e in groups:
+        rd, wr = set(), cols(tab[b])
+        for k in range(b, e):
+            r = tab[k]
+            rd |= set(int(c) for c in in_cols[int(r[S_INOFF]):int(r[S_INOFF]) + int(r[S_NIN])])
+            if int(r[S_ROLE]) == ROLE_FIXED:
+                rd |= cols(r)
+        reads.append(rd)
+        writes.append(wr)
+    level = []
+    for g in range(len(groups)):
+        lv = 0
+        for h in range(g):
+            if writes[h] & (reads[g] | writes[g]) or reads[h] & writes[g]:
+                lv = max(lv, level[h] + 1)
+        level.append(lv)
+    n_lv = max(level) + 1 if level else 0
+    out: List[List[List[Tuple[int, int]]]] = []
+    for lv in range(n_lv):
+        mem = [g for g in range(len(groups)) if level[g] == lv]
+        load = [0] * n_waves
+        assign: List[List[int]] = [[] for _ in range(n_waves)]
+        for g in sorted(mem, key=lambda g: (-(groups[g][1] - groups[g][0]), g)):
+            w = min(range(n_waves), key=lambda w: (load[w], w))
+            assign[w].append(g)
+            load[w] += groups[g][1] - groups[g][0]
+        out.append([[groups[g] for g in sorted(a)] for a in assign])
+    if collect:
+        out.append([[(c, c + 1) for c in collect]] + [[] for _ in range(n_waves - 1)])
+    return out
