@@ -203,12 +203,17 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, one GPU per rank); gloo only to rehearse several ranks on one GPU")
     ap.add_argument("--prune-barren", action="store_true")
+    ap.add_argument("--no-precompute", action="store_true",
+                    help="recompute nodes with shared-root parents per query (A/B of plan.precompute_plans)")
     ap.add_argument("--exact-f32", action="store_true", help="hidden layer on the exact f32 MFMA chain")
     ap.add_argument("--kde-valu", action="store_true", help="KDE distances on packed VALU (default: 16x16x4 f32 MFMA tile)")
     ap.add_argument("--plan-jit", choices=("auto", "on", "off"), default="auto",
                     help="plan-specialised walk kernel (hiprtc, vectorizedbayesiannetwork_amd/jit.py) or the "
                          "step-table interpreter")
     args = ap.parse_args()
+    if args.no_precompute:
+        from vectorizedbayesiannetwork_amd import engines as _E
+        _E.PRECOMPUTE = False
     if args.cpu_baseline_child:                       # fresh process, never touches the GPU
         cpu_baseline_child(args.config, args.cpu_queries, args.cpu_reps)
         return
@@ -283,6 +288,13 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / reps
     assert bool(ops.LAST_WALK.get("specialised")) == specialised, "kernel timing ran another walk form"
     kernel_name = "vbn_walk_plan" if specialised else "vbn_walk_kernel"
+    precomputed = bool(E.LAST_LAUNCH.get("precomputed"))
+    n_precomp = 0
+    if precomputed:
+        # nodes with shared-root parents computed once per sample: the HIP-event interval holds
+        # the one-query pre-pass launch as well as the walk (plan.precompute_plans)
+        kernel_name += " + shared-sample pre-pass (vbn_walk_kernel, 1 query)"
+        n_precomp = int(((plan.pc.steps[:, 2] & 8192) != 0).sum().item())
 
     for _ in range(args.warmup):
         vbn.infer_posterior(query)
@@ -364,7 +376,8 @@ def main():
                    "walk": ("plan-specialised (step table compiled in with hiprtc)" if specialised
                             else "step-table interpreter"),
                    "plan_compile_s": round(jit.STATS["compile_s"], 2), "plan_cache_hits": jit.STATS["disk_hits"],
-                   "first_call_s": round(t_first, 2)},
+                   "first_call_s": round(t_first, 2),
+                   "shared_sample_precompute_nodes": n_precomp},
         "roofline": roof,
     }
     if fallbacks:

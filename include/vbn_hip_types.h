@@ -58,6 +58,15 @@ enum vbn_role {
 #define VBN_F_HEAD_MFMA 4096    /* NN CPD head (8..32 outputs) on the split-f16 MFMA like layer 2:
                                    reserved[2] = its fragments [hi 2][64][8 f16] ++ [lo ...]
                                    (1024 floats), then the accumulator-init bias [2][16]      */
+#define VBN_F_PRECOMP 8192      /* per-sample quantities of a node whose parents are all shared
+                                   root draws (MCM / LW / ancestral, Q5), computed once per sample
+                                   by a one-query pre-pass walk and read from state (state_flags
+                                   4; state = the pre-pass out_x [S][stride], aux2 = first column
+                                   | stride << 16):  NN CPDs  the n_out MLP head outputs (the MLP
+                                   is skipped);  kde (LATENT)  the 16 inverse-CDF chunk sums ++
+                                   the underflow shift (pass 1 is skipped)                    */
+#define VBN_F_PRE_OUT 16384     /* the pre-pass step of such a node: write those quantities to
+                                   out_col .. (NN: n_out, kde: 17 slots) instead of a sample  */
 
 /* activations of the NN CPDs (reference gaussian_nn.py:19-24) */
 enum vbn_act { VBN_ACT_RELU = 0, VBN_ACT_TANH = 1, VBN_ACT_GELU = 2, VBN_ACT_ELU = 3 };
@@ -121,7 +130,9 @@ typedef struct vbn_walk_args {
   float* state;            /* optional particle state [n_slots + 1][B*S] (slot-major; the
                               last row is the log-weight accumulator) for walks split into
                               segments (resampled importance sampling)                 */
-  int32_t state_flags;     /* 1: load slots + log-weight from state before the first step;
+  int32_t state_flags;     /* 4 (alone; lean walks): state holds the per-sample quantities of
+                              the VBN_F_PRECOMP steps, read-only;
+                              1: load slots + log-weight from state before the first step;
                               2: store them after the last step                        */
   int32_t gibbs_iters;     /* Gibbs sweeps (mode GIBBS; burn_in + n_collect * thin)   */
   int32_t gibbs_burn_in;

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Precompile the plan-specialised walks of the benchmark workloads on the build host (CPU,
+hiprtc) into the package's plan cache (vectorizedbayesiannetwork_amd/plan_cache), so a fresh
+GPU box loads them instead of compiling inside the first call.
+
+    python scripts/precompile_plans.py [cfg2 cfg3 ...]        (default: every bench config)
+
+Per config: the bench engine's production plan (MCM / IS / LW) and, for shared-root engines,
+its shared-sample precompute variant (plan.precompute_plans) -- the same step tables the
+engines build, so the cache keys match.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def plans_for(cfg_name):
+    import bench
+    from vectorizedbayesiannetwork_amd import plan as P
+    cfg, model, target, ev = bench.build_model(cfg_name)
+    pk = P.PackedModel(model, "cpu")
+    vals = set(ev)
+    fixed = [x for x in model.topo if x in vals]
+    latent = [x for x in model.topo if x not in vals]
+    eng = cfg["engine"]
+    if eng == "importance_sampling":
+        plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[x for x in model.topo if x in vals],
+                            out_nodes=[target], shared_roots=False, mode=P.MODE_WEIGHTED, skip=[])
+    elif eng == "monte_carlo_marginalization":
+        plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[target], out_nodes=[target],
+                            shared_roots=True, mode=P.MODE_MCM, skip=[])
+    else:
+        return cfg, []
+    out = [("plain", plan, False)]
+    pc = P.precompute_plans(pk, plan) if eng != "importance_sampling" else None
+    if pc is not None:
+        out.append(("precompute", pc[0], True))
+    return cfg, out
+
+
+def main(names):
+    from vectorizedbayesiannetwork_amd import jit, synthetic
+    names = names or ["cfg2", "cfg3", "cfg4", "cfg5", "anchor64"]
+    for name in names:
+        if name not in synthetic.CONFIGS:
+            raise SystemExit(f"unknown config {name}")
+        cfg, plans = plans_for(name)
+        for tag, plan, pre in plans:
+            t0 = time.perf_counter()
+            key, comp = jit.precompile(plan, cfg["B"], cfg["S"], precomp=pre)
+            print(f"{name} {tag}: {key} ({'compiled' if comp else 'cached'} in {time.perf_counter() - t0:.1f} s)",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

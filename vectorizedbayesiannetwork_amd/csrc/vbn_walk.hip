@@ -320,6 +320,9 @@ static int walk_shape(const vbn_walk_args* a, walk_launch* out) {
     return fail(VBN_E_ARGS, "vbn_hip_walk: bad arguments");
   if (a->out_x && (!a->out_cols || a->n_out_cols <= 0))
     return fail(VBN_E_ARGS, "vbn_hip_walk: out_x without out_cols");
+  if ((a->state_flags & 4) && (!a->state || a->state_flags != 4 || a->noise || a->mode == VBN_MODE_GIBBS))
+    return fail(VBN_E_ARGS, "vbn_hip_walk: state_flags 4 (precomputed per-sample quantities) needs a state "
+                            "buffer and a walk without injected draws, segments or Gibbs sweeps");
   if (a->wbuf_floats < 0 || (a->wbuf_floats % WBLK_CHUNK) != 0)
     return fail(VBN_E_ARGS, "vbn_hip_walk: wbuf_floats must be a non-negative multiple of 256");
   if (a->wave_particles != 0 && a->wave_particles != 32 && a->wave_particles != WAVE)
@@ -377,7 +380,9 @@ static int walk_shape(const vbn_walk_args* a, walk_launch* out) {
   const int64_t blocks = (total + wp * nw - 1) / (wp * nw);
   if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
   // kind set | 64: the half-wave (mirror) instantiation; | 128: the lean one
-  const bool lean = !a->noise && !a->state && a->mode != VBN_MODE_GIBBS;
+  // lean: no injected draws, no segment state (state_flags 4 = read-only per-sample quantities
+  // of VBN_F_PRECOMP steps, which the lean walk reads), not Gibbs
+  const bool lean = !a->noise && (!a->state || a->state_flags == 4) && a->mode != VBN_MODE_GIBBS;
   out->kmi = km | (wp == 32 ? 64u : 0u) | (lean && wp != 32 ? 128u : 0u) |
              (wp == 32 && !a->noise ? 256u : 0u) |  // | 256: half-wave without injected draws
              (generic ? 512u : 0u);                 // | 512: with the generic-MLP path

@@ -212,6 +212,13 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
   return A.fixed[row * A.fixed_ld + st.fixed_col + d];
 }
 
+// VBN_F_PRECOMP: this sample's row of the node's pre-pass quantities (state_flags 4: state =
+// the one-query pre-pass walk's out_x [S][stride]; aux2 = first column | stride << 16)
+__device__ __forceinline__ const float* precomp_row(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  const int col = st.aux2 & 0xffff, stride = (int)((unsigned)st.aux2 >> 16);
+  return A.state + (int64_t)L.s * stride + col;
+}
+
 // value of a fixed node: from the fixed buffer, or (VBN_F_KEEP, Gibbs) the slot's current value
 __device__ __forceinline__ float node_fixed(const vbn_walk_args& A, const vbn_step& st, int d,
                                             const Lane& L) {
@@ -717,6 +724,13 @@ __device__ __forceinline__ void run_mlp_generic(const vbn_walk_args& A, const vb
 template <unsigned KM, int NOUT = 0, typename F>
 __device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
   constexpr bool MIR = (KM & 64) != 0;             // half-wave instantiation
+  if (st.flags & VBN_F_PRECOMP) {                  // parents = shared root draws: this sample's
+    const float* __restrict__ q = precomp_row(A, st, L);   // head outputs from the pre-pass
+    pre();
+    for (int j = 0; j < st.n_out; ++j) L.scr[j * WAVE + L.lane] = q[j];
+    wave_sync();
+    return;
+  }
   if constexpr ((KM & 512) != 0) {                 // kind-set bit 9: plans with generic MLPs
     if (st.flags & VBN_F_MLP_GENERIC) {            // hidden_dims other than (32, 32)
       pre();
@@ -1376,6 +1390,17 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   double tot = 0.0;
   float xv[4] = {0.f, 0.f, 0.f, 0.f};
   const float negsq = kde_own(L, slots, scl, nf, xv);
+  const bool pre = (st.flags & VBN_F_PRECOMP) != 0;
+  float shift = 0.f;
+  if (pre) {                                          // pass 1 of this sample from the pre-pass
+    const float* __restrict__ q = precomp_row(A, st, L);
+    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+      const float cs = q[ch];
+      L.scr[ch * WAVE + lane] = cs;
+      tot += (double)cs;
+    }
+    shift = q[KDE_CHUNKS];
+  } else
 #ifdef VBN_ABL_NOP1
   if (true) {
     for (int ch = 0; ch < KDE_CHUNKS; ++ch) { L.scr[ch * WAVE + lane] = 1.f; tot += 1.0; }
@@ -1410,8 +1435,7 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
   // per-point records (4 weight-0 rows before the first point), then the reversed copy
   const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
-  float shift = 0.f;
-  if (!(tot > 0.0)) {                                 // every weight underflowed (or NaN parent)
+  if (!pre && !(tot > 0.0)) {                         // every weight underflowed (or NaN parent)
     float amax = -INFINITY;
     for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nfr));
     shift = amax;
@@ -1424,6 +1448,12 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
       L.scr[ch * WAVE + lane] = cs;
       tot += (double)cs;
     }
+  }
+  if (st.flags & VBN_F_PRE_OUT) {                    // pre-pass: pass 1's result is the output
+    for (int c = 0; c < KDE_CHUNKS; ++c) vwrite(L, st.out_col + c, L.scr[c * WAVE + lane]);
+    vwrite(L, st.out_col + KDE_CHUNKS, shift);
+    wave_sync();
+    return -1;
   }
   const double thr = (double)ucat * tot;
   double cum = 0.0;
@@ -1610,6 +1640,7 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
           : (st.aux0 == 2 ? kde_index_valu<2>(A, st, L, ucat, c_p) : kde_index_valu<3>(A, st, L, ucat, c_p));
     } else if (st.reserved[1] >= 0) {
       idx = kde_index_mfma(A, st, L, ucat, c_p);
+      if (st.flags & VBN_F_PRE_OUT) return;            // pre-pass: sums written, no sample
     } else {
       // pass 1: per-chunk weight sums -> scr[chunk][lane]
       const int csz = (M + KDE_CHUNKS - 1) / KDE_CHUNKS;
@@ -1784,6 +1815,15 @@ __device__ __forceinline__ void walk_step(const vbn_walk_args& A, const vbn_step
   }
   if (!L.lean && st.role == VBN_ROLE_COLLECT) {
     gibbs_collect(A, st, L);
+    return;
+  }
+  if ((st.flags & VBN_F_PRE_OUT) && st.kind != VBN_KIND_KDE) {   // shared-sample pre-pass: the
+    if constexpr ((KM & 21u) != 0) {                                 // NN CPD's head outputs
+      if (st.kind == VBN_KIND_GAUSSIAN_NN && st.out_dim == 1) run_mlp<KM, 2>(A, st, L, [] {});
+      else run_mlp<KM>(A, st, L, [] {});
+      for (int j = 0; j < st.n_out; ++j) vwrite(L, st.out_col + j, L.scr[j * WAVE + L.lane]);
+    }
+    wave_sync();
     return;
   }
   if (st.role == VBN_ROLE_FIXED && !(st.flags & VBN_F_LOGP)) {   // evidence / do: value only

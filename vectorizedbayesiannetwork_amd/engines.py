@@ -41,6 +41,7 @@ import torch
 from . import ops
 from .model import BNModel, model_from_vbn
 from .plan import (MODE_MCM, MODE_SAMPLE, MODE_WEIGHTED, GibbsPlan, PackedModel, QueryPlan, barren_pruned,
+                   precompute_plans,
                    build_gibbs_plan, build_plan)
 from .registry import register_inference, register_sampling
 
@@ -113,8 +114,19 @@ def _plan(pk: PackedModel, key, **kw) -> QueryPlan:
     p = pk.model._cache.get(ck)
     if p is None:
         p = build_plan(pk, **kw)
+        if kw.get("shared_roots") and not kw.get("params"):
+            # shared root draws: nodes whose parents are all roots are computed once per sample
+            pc = precompute_plans(pk, p, skip=kw.get("skip", ()), exact_f32=kw.get("exact_f32", False),
+                                  kde_valu=kw.get("kde_valu", False))
+            if pc is not None:
+                p.pc, p.pre = pc
         pk.model._cache[ck] = p
     return p
+
+
+# shared-sample precompute (plan.precompute_plans) in production walks; False: every node per
+# particle (A/B, tests)
+PRECOMPUTE = True
 
 
 def _fixed_values(query, device, clamp: bool = False) -> Dict[str, torch.Tensor]:
@@ -204,14 +216,26 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
         noise_b = int(noise.shape[2])
         if noise.shape[3] != n or noise.shape[4] != pk.dmax:
             raise ValueError(f"noise must be [n_latent, 2, B|1, {n}, {pk.dmax}]")
+    precomp = None
+    walk_plan = plan
+    if (PRECOMPUTE and plan.pc is not None and noise is None and state is None and step_begin == 0
+            and step_end < 0 and n % 64 == 0 and not fixed_per_particle):
+        # the per-sample quantities of nodes with shared-root parents, once per sample (same
+        # seed / offset: the pre-pass draws the main walk's root values), then the main walk
+        _, precomp = run_walk(pk, plan.pre, fixed, 1, n, seed=seed, offset=offset, plan_jit=0)
+        precomp = precomp.view(n, -1)
+        walk_plan = plan.pc
+    # (the plan as given: a re-run of this launch repeats the pre-pass)
     LAST_LAUNCH.update(pk=pk, plan=plan, fixed=fixed, b=b, n=n, fixed_per_particle=fixed_per_particle,
-                       noise=noise, state=state, seed=seed, offset=offset, plan_jit=plan_jit)
+                       noise=noise, state=state, seed=seed, offset=offset, plan_jit=plan_jit,
+                       precomputed=precomp is not None)
+    plan = walk_plan
     args = (plan.steps, plan.in_cols, pk.params, fixed, noise, plan.out_cols, b, n,
             plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
             len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
             plan.mode != MODE_SAMPLE, plan.kind_mask)
     if state is None:
-        lp, x = ops.walk(*args, plan.wbuf, plan_jit)
+        lp, x = ops.walk(*args, plan.wbuf, plan_jit, precomp)
     else:
         lp, x = ops.walk_segment(*args, state, state_flags, step_begin, step_end, plan.wbuf)
     if plan.mode != MODE_SAMPLE:

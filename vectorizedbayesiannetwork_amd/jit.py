@@ -9,8 +9,9 @@ launches it with the same arguments, grid and LDS as the interpreter
 (``vbn_hip_walk_module``): same device functions, same operation order, bit-identical
 outputs, no per-step loads or dispatch (cfg2 walk 1.01 -> 0.88 ms, cfg3 3.83 -> 3.05 ms).
 
-Compiled code objects are cached per process and on disk (``$VBN_HIP_CACHE``, default
-``~/.cache/vbn_hip``), keyed by the source, the options and the hiprtc version.  Only lean
+Compiled code objects are cached per process and on disk (``$VBN_HIP_CACHE``, default the
+package's ``plan_cache/``, which ``scripts/precompile_plans.py`` fills on the build host for the
+benchmark workloads), keyed by the source, the options, the hiprtc version and the headers.  Only lean
 full-wave walks are specialised (production MCM / IS / LW / ancestral); by default only
 launches of at least ``JIT_MIN_PARTICLES`` particles (a compile takes seconds) --
 ``VBN_PLAN_JIT=0`` disables it, the engines' ``plan_jit=True`` forces it.  Without hiprtc, or
@@ -136,7 +137,9 @@ def compile_source(src: str) -> bytes:
 
 
 def _cache_dir() -> Optional[str]:
-    d = os.environ.get("VBN_HIP_CACHE") or os.path.join(os.path.expanduser("~"), ".cache", "vbn_hip")
+    # default: in the package tree, so code objects precompiled on the build host
+    # (scripts/precompile_plans.py, __graft_entry__.build) travel with the built library
+    d = os.environ.get("VBN_HIP_CACHE") or os.path.join(HERE, "plan_cache")
     try:
         os.makedirs(d, exist_ok=True)
         return d if os.access(d, os.W_OK) else None
@@ -225,3 +228,39 @@ def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_ind
                       file=sys.stderr)
                 _warned = True
             return None
+
+
+def walk_kind_set(plan, n_queries: int, n_samples: int, precomp: bool = False, wave_particles: int = 0) -> int:
+    """The kind-set instantiation a lean launch of ``plan`` runs (host only: the C-ABI's
+    vbn_hip_walk_kind_set on a descriptor with placeholder pointers)."""
+    lib = _lib.load()
+    a = _lib.VbnWalkArgs()
+    a.steps = 16                                   # placeholders: the shape logic never dereferences
+    a.params = 16
+    a.in_cols = 16
+    a.n_queries = n_queries
+    a.n_samples = n_samples
+    a.n_steps = plan.n_steps
+    a.n_slots = plan.n_slots
+    a.max_out = plan.max_out
+    a.mode = plan.mode
+    a.kind_mask = plan.kind_mask
+    a.wbuf_floats = int(plan.wbuf)
+    a.wave_particles = wave_particles
+    if precomp:
+        a.state = 16
+        a.state_flags = 4
+    km = lib.vbn_hip_walk_kind_set(ctypes.byref(a))
+    if km <= 0:
+        _lib.check(-km if km < 0 else 1, "vbn_hip_walk_kind_set")
+    return km
+
+
+def precompile(plan, n_queries: int, n_samples: int, precomp: bool = False) -> Tuple[str, float]:
+    """Compile (or find in the disk cache) the specialised walk of a lean launch of ``plan``;
+    returns (cache key, seconds spent compiling)."""
+    km = walk_kind_set(plan, n_queries, n_samples, precomp)
+    steps, ic, _ = plan.steps._vbn_host
+    t0 = STATS["compile_s"]
+    key, _ = code_object(steps, ic, km)
+    return key, STATS["compile_s"] - t0

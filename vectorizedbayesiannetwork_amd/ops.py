@@ -44,14 +44,25 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
          out_cols: Tensor, n_queries: int, n_samples: int, n_slots: int, max_out: int,
          fixed_ld: int, fixed_per_particle: bool, noise_b: int, n_noise: int, dmax: int,
          n_out_cols: int, mode: int, q_base: int, seed: int, offset: int,
-         want_lp: bool, kind_mask: int = 63, wbuf: int = 0, plan_jit: int = 1) -> Tuple[Tensor, Tensor]:
+         want_lp: bool, kind_mask: int = 63, wbuf: int = 0, plan_jit: int = 1,
+         precomp: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
     """One particle walk over the whole step table (``wbuf``: floats per LDS weight buffer,
     >= every step's weight-block length).  ``plan_jit``: 0 = step-table interpreter, 1 = the
     plan-specialised walk (jit.py) for lean launches of >= jit.JIT_MIN_PARTICLES particles,
-    2 = for every lean launch."""
+    2 = for every lean launch.  ``precomp``: the per-sample quantities of the table's
+    VBN_F_PRECOMP steps ([S, stride], the pre-pass walk's out_x; plan.precompute_plans)."""
+    if precomp is not None:
+        if noise is not None:
+            raise ValueError("vbn_hip::walk: precomputed quantities need a walk without injected draws")
+        if precomp.dim() != 2 or precomp.shape[0] != n_samples:
+            raise ValueError(f"vbn_hip::walk: precomp must be [{n_samples}, stride], got {tuple(precomp.shape)}")
+        need = getattr(steps, "_vbn_precomp_stride", None)
+        if need is not None and precomp.shape[1] != need:
+            raise ValueError(f"vbn_hip::walk: precomp has {precomp.shape[1]} columns, the step table reads {need}")
     return _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots,
                         max_out, fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode,
-                        q_base, seed, offset, want_lp, kind_mask, None, 0, 0, -1, wbuf, plan_jit)
+                        q_base, seed, offset, want_lp, kind_mask, precomp, 4 if precomp is not None else 0,
+                        0, -1, wbuf, plan_jit)
 
 
 @torch.library.custom_op("vbn_hip::walk_segment", mutates_args=("state",))
@@ -112,7 +123,7 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
         if state is None:
             raise ValueError("vbn_hip::walk: state_flags without a state buffer")
         _check_dev("state", state, torch.float32, device)
-        if state.numel() < (n_slots + 1) * total:
+        if state_flags & 3 and state.numel() < (n_slots + 1) * total:
             raise ValueError(f"vbn_hip::walk: state has {state.numel()} values, needs {(n_slots + 1) * total}")
     rows = total if fixed_per_particle else n_queries
     if fixed.numel() < rows * fixed_ld:
@@ -190,7 +201,7 @@ def _plan_module(lib, a, steps, step_begin, step_end, work, plan_jit, device, ch
 @walk.register_fake
 def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
-               offset, want_lp, kind_mask=63, wbuf=0, plan_jit=1):
+               offset, want_lp, kind_mask=63, wbuf=0, plan_jit=1, precomp=None):
     total = n_queries * n_samples
     lp = params.new_empty(total if want_lp else 0)
     x = params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))

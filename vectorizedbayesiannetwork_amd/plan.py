@@ -46,6 +46,8 @@ KDE_REC_TAIL = 8       # weight-0 record rows after the last point (csrc kde_sca
 MLP_HIDDEN = (32, 32)
 HEAD_MFMA_MIN = 8         # heads at least this wide run on MFMA (csrc head_mfma)
 F_HEAD_MFMA = 4096
+F_PRECOMP = 8192          # csrc VBN_F_PRECOMP: per-sample quantities read from the pre-pass
+F_PRE_OUT = 16384         # csrc VBN_F_PRE_OUT: the pre-pass writes a node's per-sample quantities
 MAX_NODES = 1 << 14
 MAX_NODE_DIMS = 1 << 8
 
@@ -438,6 +440,10 @@ class QueryPlan:
     kind_mask: int = 63       # CPD kinds the walk evaluates (selects the kernel instantiation;
                               # | 32 non-relu activations, | 512 generic-MLP nodes)
     wbuf: int = 0             # floats per LDS weight buffer (max wblk_len over the steps)
+    # shared-sample precompute (precompute_plans): the same walk with VBN_F_PRECOMP steps, and
+    # the one-query pre-pass walk whose out_x they read
+    pc: Optional["QueryPlan"] = None
+    pre: Optional["QueryPlan"] = None
 
 
 def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
@@ -456,7 +462,7 @@ def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
 def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[str],
                logp: Sequence[str], out_nodes: Sequence[str], shared_roots: bool, mode: int,
                skip: Sequence[str] = (), exact_f32: bool = False, kde_valu: bool = False,
-               params: Sequence[str] = ()) -> QueryPlan:
+               params: Sequence[str] = (), pre_out: Sequence[str] = ()) -> QueryPlan:
     """Step table for one query signature.
 
     ``latent``: nodes sampled; ``fixed``: nodes read from the fixed buffer (evidence/do);
@@ -467,11 +473,15 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
     ``params``: nodes whose conditional parameters are written instead of a draw (role
     PARAMS; gaussian_nn / linear_gaussian: loc ++ scale, softmax_nn: class probabilities
     [D][C], mdn: softmax(logits) [K] ++ loc [K][D] ++ scale [K][D]) -- the Rao-Blackwellized
-    target and CPDHandle.conditional.
+    target and CPDHandle.conditional.  ``pre_out``: latent nodes that write their per-sample
+    quantities instead of a sample (VBN_F_PRE_OUT, the shared-sample pre-pass of
+    :func:`precompute_plans`): NN CPDs their n_out MLP head outputs, KDE its 16 inverse-CDF
+    chunk sums ++ the underflow shift.
     """
     model = packed.model
     latent_s, fixed_s, logp_s, skip_s = set(latent), set(fixed), set(logp), set(skip)
     params_s = set(params)
+    pre_s = set(pre_out)
     order = [n for n in model.topo if n not in skip_s]
     for n in order:
         if n in params_s:
@@ -482,6 +492,8 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
             raise ValueError(f"node {n} must be exactly one of latent/fixed")
 
     def width(n: str) -> int:
+        if n in pre_s:
+            return precompute_width(packed, n)
         if n not in params_s:
             return model.out_dim(n)
         rec = model.cpds[n]
@@ -557,6 +569,8 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
             fl |= F_F32L2
         if kde_valu and npk.kind == KIND_ID["kde"]:
             fl |= F_KDE_VALU
+        if n in pre_s:
+            fl |= F_PRE_OUT
         row[S_FLAGS] = fl
         row[S_ACT] = npk.act
         row[S_NIN] = npk.n_in
@@ -795,3 +809,89 @@ def gibbs_levels(tab: np.ndarray, in_cols: np.ndarray, n_waves: int) -> List[Lis
     if collect:
         out.append([[(c, c + 1) for c in collect]] + [[] for _ in range(n_waves - 1)])
     return out
+
+
+
+def precompute_width(packed: PackedModel, n: str) -> int:
+    """Per-sample quantities of a precomputed node: NN CPDs their MLP head outputs, KDE its 16
+    inverse-CDF chunk sums ++ the underflow shift."""
+    npk = packed.nodes[n]
+    return KDE_CHUNKS + 1 if npk.kind == KIND_ID["kde"] else int(npk.n_out)
+
+
+def precompute_plans(packed: PackedModel, plan: QueryPlan, *, skip: Sequence[str] = (),
+                     exact_f32: bool = False, kde_valu: bool = False) -> Optional[Tuple[QueryPlan, QueryPlan]]:
+    """Shared-sample precompute of a walk with shared root draws (MCM / LW / ancestral, Q5).
+
+    The root draws are shared by every query of the batch, so a node whose parents are all
+    latent roots sees the same inputs in every query of a sample: its MLP head outputs
+    (gaussian_nn, mdn, softmax_nn) or its KDE inverse-CDF chunk sums depend on the sample only.
+    A one-query pre-pass walk (the same root steps -- same flags, so the same Philox draws and
+    Box-Muller pairs -- then those nodes with VBN_F_PRE_OUT) computes them once per sample; the
+    main walk's steps for those nodes (VBN_F_PRECOMP) read them instead of recomputing them per
+    query, then run their epilogue and per-query draws as before.  Same device functions on
+    the same values: the outputs are bit-identical to the plain walk when every wave holds one
+    query (S a multiple of 64: the MLP's wave-uniform exact-path decision then sees the same
+    particles; run_walk checks).  Returns (main plan with VBN_F_PRECOMP, pre-pass plan), or
+    None when no node qualifies.
+    """
+    model = packed.model
+    rows = plan.steps._vbn_host[0].copy()
+    order = [n for n in model.topo if n not in set(skip)]
+    assert len(order) == len(rows)
+    at = {n: i for i, n in enumerate(order)}
+    roots = [n for n in order if rows[at[n]][S_ROLE] == ROLE_LATENT and rows[at[n]][S_FLAGS] & F_SHARED]
+    root_s = set(roots)
+    nn_kinds = (KIND_ID["gaussian_nn"], KIND_ID["mdn"], KIND_ID["softmax_nn"])
+    cand = []
+    for n in order:
+        r = rows[at[n]]
+        if r[S_FLAGS] & (F_ROOT | F_SHARED) or not model.parents[n]:
+            continue
+        if not all(p in root_s for p in model.parents[n]):
+            continue
+        kind, role = int(r[S_KIND]), int(r[S_ROLE])
+        if kind in nn_kinds and not r[S_FLAGS] & F_MLP_GENERIC and (
+                role == ROLE_LATENT or (role == ROLE_FIXED and r[S_FLAGS] & F_LOGP)):
+            cand.append(n)
+        elif (kind == KIND_ID["kde"] and role == ROLE_LATENT and not r[S_FLAGS] & F_KDE_VALU
+              and r[S_OFF_KQ] >= 0):
+            cand.append(n)
+    if not cand:
+        return None
+    keep = root_s | set(cand)
+    pre = build_plan(packed, latent=roots + cand, fixed=[], logp=[], out_nodes=cand, shared_roots=True,
+                     mode=MODE_SAMPLE, skip=[n for n in model.topo if n not in keep], exact_f32=exact_f32,
+                     pre_out=cand)
+    prow = pre.steps._vbn_host[0].copy()
+    porder = [n for n in model.topo if n in keep]
+    for i, n in enumerate(porder):                   # the main walk's Box-Muller pairs (roots pair
+        prow[i][S_FLAGS] &= ~(F_BM_FIRST | F_BM_SECOND)            # with roots only) and no others
+        if n in root_s:
+            prow[i][S_FLAGS] |= rows[at[n]][S_FLAGS] & (F_BM_FIRST | F_BM_SECOND)
+    pre = _with_steps(pre, prow, packed.device)
+    stride = int(pre.out_cols.numel())
+    col = 0
+    for n in cand:
+        r = rows[at[n]]
+        r[S_FLAGS] |= F_PRECOMP
+        r[S_AUX2] = col | (stride << 16)
+        col += precompute_width(packed, n)
+        r[S_WBLK_OFF] = 0                            # no MLP runs: nothing to stage
+        r[S_WBLK_LEN] = 0
+    assert col == stride and stride < (1 << 15)
+    return _with_steps(plan, rows, packed.device), pre
+
+
+def _with_steps(plan: QueryPlan, rows: np.ndarray, device) -> QueryPlan:
+    """A copy of ``plan`` with another step table (same slots, parent lists and outputs)."""
+    import dataclasses
+    steps_t = torch.from_numpy(np.ascontiguousarray(rows)).to(device)
+    steps_t._vbn_wblk_max = int(rows[:, S_WBLK_LEN].max()) if len(rows) else 0
+    pcm = (rows[:, S_FLAGS] & F_PRECOMP) != 0
+    if pcm.any():                                    # ops.walk checks the precomp tensor's width
+        steps_t._vbn_precomp_stride = int(rows[pcm, S_AUX2][0]) >> 16
+    ic_host = plan.steps._vbn_host[1]
+    steps_t._vbn_host = (rows.copy(), ic_host.copy(),
+                         hashlib.sha1(rows.tobytes() + b"|" + ic_host.tobytes()).hexdigest())
+    return dataclasses.replace(plan, steps=steps_t, wbuf=steps_t._vbn_wblk_max, pc=None, pre=None)
