@@ -2,7 +2,6 @@
 # round 3: shared-sample precompute (parity + A/B benches), MFMA-head A/B on cfg3
 set -o pipefail
 mkdir -p gpurun_out
-export VBN_HIP_CACHE=/tmp/vbn_hip_cache
 timeout -k 10 900 python -u -m pytest tests/test_gpu_precompute.py tests/test_gpu_jit.py -q -rs --timeout 600 --timeout-method thread > gpurun_out/r03o_pytest_gpu.txt 2>&1; rc=$?
 tail -6 gpurun_out/r03o_pytest_gpu.txt
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
