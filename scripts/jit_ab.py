@@ -63,7 +63,7 @@ def main():
     captured = {}
     orig = J.module_for
 
-    def capture(steps, in_cols, kind_set, dev, key):
+    def capture(steps, in_cols, kind_set, dev, key, *rest):
         captured["km"] = kind_set
         return None
     J.module_for = capture

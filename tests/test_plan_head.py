@@ -5,7 +5,7 @@ import pytest
 
 from vectorizedbayesiannetwork_amd import synthetic
 from vectorizedbayesiannetwork_amd.model import random_init_model
-from vectorizedbayesiannetwork_amd.plan import (F_HEAD_MFMA, HEAD_MFMA_MIN, MODE_WEIGHTED, S_FLAGS, S_KIND,
+from vectorizedbayesiannetwork_amd.plan import (F_HEAD_MFMA, MODE_WEIGHTED, S_FLAGS, S_KIND,
                                                 S_NOUT, S_OFF_KQ, S_OFF_KQY, PackedModel, _ROWS, build_plan)
 
 
@@ -22,7 +22,10 @@ def _plan(model, pk):
                       out_nodes=[topo[0]], shared_roots=False, mode=MODE_WEIGHTED)
 
 
-def test_wide_heads_carry_mfma_fragments():
+def test_wide_heads_carry_mfma_fragments(monkeypatch):
+    import vectorizedbayesiannetwork_amd.plan as P
+    monkeypatch.setattr(P, "HEAD_MFMA_MIN", 8)     # the packing of the (optional) MFMA head
+    HEAD_MFMA_MIN = 8
     model = _model()
     pk = PackedModel(model, "cpu")
     plan = _plan(model, pk)
