@@ -95,21 +95,27 @@ def test_lean_mcm_matches_oracle(cfg_name):
     _check(f"{cfg_name} MCM", bad_x | bad_p, draws, (B_PARITY, S_PARITY))
 
 
+@pytest.mark.parametrize("plan_jit", [False, True])
 @pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3"])
 @pytest.mark.parametrize("engine", ["importance_sampling", "likelihood_weighting"])
-def test_lean_weighted_walk_matches_oracle(cfg_name, engine):
+def test_lean_weighted_walk_matches_oracle(cfg_name, engine, plan_jit):
     """IS (per-query root draws, raw evidence) and LW (shared roots, clamped evidence)
-    log-weights and target samples per particle, before normalisation."""
+    log-weights and target samples per particle, before normalisation; step-table interpreter
+    and plan-specialised kernel (the latter pinned here directly: with split-f16 MFMA heads its
+    evidence log-weights are not bitwise the interpreter's, test_gpu_jit.py)."""
     from vectorizedbayesiannetwork_amd import engines as E
     from vectorizedbayesiannetwork_amd.engines import ImportanceSampling, LikelihoodWeighting, Query
     model, vbn, target, ev = _workload(cfg_name, B_PARITY)
     seed = 77001
     q = Query(target, {k: v.cuda() for k, v in ev.items()})
     is_ = engine == "importance_sampling"
-    eng = ImportanceSampling(n_samples=S_PARITY) if is_ else LikelihoodWeighting(n_samples=S_PARITY)
+    cls = ImportanceSampling if is_ else LikelihoodWeighting
+    eng = cls(n_samples=S_PARITY, plan_jit=plan_jit)
     log_w, xs = eng._walk(vbn, q, S_PARITY, clamp=not is_, shared_roots=not is_,
                           kwargs={"_seed_value": seed})
     torch.cuda.synchronize()
+    from vectorizedbayesiannetwork_amd import ops
+    assert bool(ops.LAST_WALK.get("specialised")) == plan_jit
     last = E.LAST_LAUNCH
     assert last["noise"] is None and last["state"] is None
     draws = _provider(last["plan"], last["pk"], seed, B_PARITY, S_PARITY)

@@ -44,11 +44,12 @@ WBLK_CHUNK = 256          # floats per LDS-DMA wave instruction (64 lanes x 16 B
 KDE_CHUNKS = 16
 KDE_REC_TAIL = 8       # weight-0 record rows after the last point (csrc kde_scan prefetch)
 MLP_HIDDEN = (32, 32)
-# heads at least this wide run on the split-f16 MFMA (csrc head_mfma).  Off by default: the
-# hiprtc-compiled (plan-specialised) and hipcc-compiled (interpreter) MFMA heads give IS / LW
-# log-weights that differ by up to 3e-5 relative on evidence steps (both within the oracle
-# tolerance, profiles/r03n_headmfma_diag.txt), which breaks their bit identity; 8 enables it
-HEAD_MFMA_MIN = 1 << 30
+# heads at least this wide run on the split-f16 MFMA (csrc head_mfma; cfg3 walk 2.97 -> 2.74 ms,
+# profiles/r03_bench/r03q_ab_cfg3.txt).  The hiprtc-compiled (plan-specialised) and
+# hipcc-compiled (interpreter) MFMA heads give IS / LW log-weights that differ by up to 3e-5
+# relative on evidence steps (profiles/r03n_headmfma_diag.txt); both are pinned to the oracle
+# per particle (tests/test_gpu_lean_parity.py).  1 << 30 turns the MFMA head off.
+HEAD_MFMA_MIN = 8
 F_HEAD_MFMA = 4096
 F_PRECOMP = 8192          # csrc VBN_F_PRECOMP: per-sample quantities read from the pre-pass
 F_PRE_OUT = 16384         # csrc VBN_F_PRE_OUT: the pre-pass writes a node's per-sample quantities
