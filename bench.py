@@ -21,6 +21,7 @@ fresh child process with the tuned glibc allocator settings of BASELINE.md.
 from __future__ import annotations
 
 import argparse
+import gc
 import glob
 import json
 import math
@@ -304,6 +305,10 @@ def main():
     # timed region: exactly K steps, barrier + synchronize on both sides (the synchronize
     # also waits for the last step's gather on RCCL's stream)
     fallbacks = []
+    # Python's cyclic GC off inside the timed region (as timeit does): a collection pause early
+    # in a short timed loop, while the host is only a step or two ahead, idles the GPU
+    gc.collect()
+    gc.disable()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -315,6 +320,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     if dist:
         t = torch.tensor([elapsed], device=device if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
