@@ -8,7 +8,9 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -rs -x --timeout 600 --tim
 tail -3 gpurun_out/r03f_pytest_gpu.txt
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke OK')" > gpurun_out/r03f_smoke.txt 2>&1 || { tail -20 gpurun_out/r03f_smoke.txt; exit 1; }
 tail -1 gpurun_out/r03f_smoke.txt
-timeout -k 10 600 python -u bench.py > gpurun_out/r03f_bench_default.json 2>gpurun_out/r03f_bench_default.err || exit 1
+timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r03f_bench_default.json 2>gpurun_out/r03f_bench_default.err || exit 1
+timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/r03f_bench_default2.json 2>/dev/null || exit 1
+cat gpurun_out/r03f_bench_default2.json
 cat gpurun_out/r03f_bench_default.json
 bash profiles/profile_round.sh gpurun_out/r03f_prof cfg2 > gpurun_out/r03f_prof.log 2>&1 || { tail -5 gpurun_out/r03f_prof.log; exit 1; }
 echo profiled
