@@ -297,6 +297,14 @@ def main():
         kernel_name += " + shared-sample pre-pass (vbn_walk_kernel, 1 query)"
         n_precomp = int(((plan.pc.steps[:, 2] & 8192) != 0).sum().item())
 
+    # the host path's own settling (caching allocator, Python-side caches) before the W warmup
+    # steps: ~50 ms of untimed infer_posterior calls, like the walks of the kernel timing above
+    # (a 20-step window right after a handful of calls measured 0.92 vs 0.82 ms per step in
+    # steady state, profiles/r03_bench/r03t_blocks.txt)
+    for _ in range(max(5, min(200, math.ceil(50.0 / kern_ms)))):
+        vbn.infer_posterior(query)
+    sharded.wait()
+    torch.cuda.synchronize()
     for _ in range(args.warmup):
         vbn.infer_posterior(query)
     sharded.wait()
