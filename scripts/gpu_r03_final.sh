@@ -4,7 +4,11 @@
 # benches with the CPU baseline
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -rs -x --timeout 600 --timeout-method thread > gpurun_out/r03f_pytest_gpu.txt 2>&1 || { tail -20 gpurun_out/r03f_pytest_gpu.txt; exit 1; }
+# heartbeat: plan compiles inside a test (hiprtc, up to ~4 min for the 128-node plans) print nothing
+(while true; do date >> gpurun_out/r03f_heartbeat.txt; sleep 50; done) &
+HB=$!
+trap "kill $HB" EXIT
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rs -x --timeout 600 --timeout-method thread > gpurun_out/r03f_pytest_gpu.txt 2>&1 || { tail -20 gpurun_out/r03f_pytest_gpu.txt; exit 1; }
 tail -3 gpurun_out/r03f_pytest_gpu.txt
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke OK')" > gpurun_out/r03f_smoke.txt 2>&1 || { tail -20 gpurun_out/r03f_smoke.txt; exit 1; }
 tail -1 gpurun_out/r03f_smoke.txt
