@@ -19,15 +19,32 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def plans_for(cfg_name):
+ENGINES = {"mcm": "monte_carlo_marginalization", "is": "importance_sampling", "lw": "likelihood_weighting",
+           "ancestral": "ancestral"}
+
+
+def plans_for(name):
+    """``cfg`` (the bench engine) or ``cfg:engine`` (mcm / is / lw / ancestral: the engines'
+    plans for the GPU tests' workloads, which share the bench configs' DAGs)."""
     import bench
     from vectorizedbayesiannetwork_amd import plan as P
+    cfg_name, _, eng_name = name.partition(":")
     cfg, model, target, ev = bench.build_model(cfg_name)
     pk = P.PackedModel(model, "cpu")
     vals = set(ev)
     fixed = [x for x in model.topo if x in vals]
     latent = [x for x in model.topo if x not in vals]
-    eng = cfg["engine"]
+    eng = ENGINES[eng_name] if eng_name else cfg["engine"]
+    if eng == "likelihood_weighting":
+        plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[x for x in model.topo if x in vals],
+                            out_nodes=[target], shared_roots=True, mode=P.MODE_WEIGHTED, skip=[])
+        pc = P.precompute_plans(pk, plan)
+        return cfg, [("plain", plan, False)] + ([("precompute", pc[0], True)] if pc else [])
+    if eng == "ancestral":
+        plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[], out_nodes=[target], shared_roots=True,
+                            mode=P.MODE_SAMPLE, skip=[])
+        pc = P.precompute_plans(pk, plan)
+        return cfg, [("plain", plan, False)] + ([("precompute", pc[0], True)] if pc else [])
     if eng == "importance_sampling":
         plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[x for x in model.topo if x in vals],
                             out_nodes=[target], shared_roots=False, mode=P.MODE_WEIGHTED, skip=[])
@@ -46,8 +63,10 @@ def plans_for(cfg_name):
 def main(names):
     from vectorizedbayesiannetwork_amd import jit, synthetic
     names = names or ["cfg2", "cfg3", "cfg4", "cfg5", "anchor64"]
+    if names == ["--tests"]:                 # the extra plans of the GPU tests' workloads
+        names = ["cfg2:is", "cfg2:lw", "cfg3:lw", "cfg3:ancestral", "cfg5:ancestral"]
     for name in names:
-        if name not in synthetic.CONFIGS:
+        if name.partition(":")[0] not in synthetic.CONFIGS or name.partition(":")[2] not in ("", *ENGINES):
             raise SystemExit(f"unknown config {name}")
         cfg, plans = plans_for(name)
         for tag, plan, pre in plans:
