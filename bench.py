@@ -92,6 +92,38 @@ def mlp_flops_per_particle(model, plan):
     return f32, hidden
 
 
+def executed_work(model, plan, B: int, S: int, precomputed: bool):
+    """(f32 FLOPs, hidden-layer FLOPs, KDE exps) the launch actually executes: with the
+    precompute, a VBN_F_PRECOMP node's MLP / KDE pass 1 runs once per sample (per-sample
+    pre-pass, S particles) or once per query (per-query pre-pass, B waves of 64 lanes) instead of
+    once per particle (plan.precompute_plans)."""
+    if not precomputed or plan.pc is None:
+        f, h = mlp_flops_per_particle(model, plan)
+        return f * B * S, h * B * S, kde_exps_per_particle(model, plan) * B * S
+    f32 = hid = exps = 0.0
+    rows = plan.pc.steps.cpu().tolist()
+    for i, row in enumerate(rows):
+        one = _RowPlan([row])
+        f, h = mlp_flops_per_particle(model, one)
+        e = kde_exps_per_particle(model, one)
+        fl = row[2]
+        if fl & 8192:                                 # precomputed: pre-pass particles only
+            n = B * 64 if fl & 32768 else S
+            kde_p1 = float(row[9]) if row[0] == KIND_ID["kde"] and row[1] == 1 else 0.0
+            f32, hid, exps = f32 + f * n, hid + h * n, exps + kde_p1 * n + (e - kde_p1) * B * S
+        else:
+            f32, hid, exps = f32 + f * B * S, hid + h * B * S, exps + e * B * S
+    return f32, hid, exps
+
+
+class _RowPlan:
+    """one step row as a plan (mlp_flops_per_particle / kde_exps_per_particle)"""
+
+    def __init__(self, rows):
+        self.steps = torch.tensor(rows, dtype=torch.int32)
+        self.n_steps = len(rows)
+
+
 def kde_exps_per_particle(model, plan) -> float:
     """Algorithmic kernel-weight evaluations (one exp each) of one particle in one walk:
     M for a sampled non-root KDE node (the CDF pass; the chunk rescan is not counted),
@@ -261,10 +293,18 @@ def main():
     from vectorizedbayesiannetwork_amd import engines as E
     from vectorizedbayesiannetwork_amd import jit, ops
     t_first = time.perf_counter()
-    vbn.infer_posterior(query)                # builds (and compiles) the plan of the timed steps
+    vbn.infer_posterior(query)                # builds the plan of the timed steps
     sharded.wait()
     torch.cuda.synchronize()
     t_first = time.perf_counter() - t_first
+    # a plan missing from the code-object cache compiles in the background (jit.py) while the
+    # first call runs the interpreter: wait for it, so every later step runs the same form
+    t_wait = time.perf_counter()
+    jit.wait_pending()
+    t_wait = time.perf_counter() - t_wait
+    vbn.infer_posterior(query)
+    sharded.wait()
+    torch.cuda.synchronize()
     specialised = bool(ops.LAST_WALK.get("specialised"))
     last = dict(E.LAST_LAUNCH)
     pk, plan, fixed = last["pk"], last["plan"], last["fixed"]
@@ -339,6 +379,37 @@ def main():
     if rank == 0 and gather:
         assert pdf is not None and pdf.shape[0] == world * B, "rank 0 must hold the gathered batch"
 
+    # the gather's cost, outside the timed region: the same steps with no gather and with a
+    # synchronous (not overlapped) gather, max over ranks; rank 0's received bytes per step
+    gather_info = None
+    if dist and gather:
+        def window(n, on, overlap):
+            sharded.gather, sharded.overlap = on, overlap
+            barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(n):
+                vbn.infer_posterior(query)
+            sharded.wait()
+            torch.cuda.synchronize()
+            barrier()
+            dt = torch.tensor([time.perf_counter() - t], dtype=torch.float64,
+                              device=device if args.dist_backend == "nccl" else "cpu")
+            tdist.all_reduce(dt, op=tdist.ReduceOp.MAX)
+            return 1e3 * float(dt.item()) / n
+        n_g = max(5, min(args.steps, 20))
+        b0 = sharded.gather_bytes
+        walk_only = window(n_g, False, False)
+        sync_gather = window(n_g, True, False)
+        per_step = (sharded.gather_bytes - b0) / n_g
+        sharded.gather, sharded.overlap = True, True
+        gather_info = {"bytes_to_rank0_per_step": int(per_step) if rank == 0 else None,
+                       "walk_only_ms_per_step": round(walk_only, 4),
+                       "sync_gather_ms_per_step": round(sync_gather, 4),
+                       "gather_ms_per_step_unoverlapped": round(sync_gather - walk_only, 4),
+                       "overlapped_ms_per_step": round(ms_per_step, 4),
+                       "steps_each": n_g}
+
     f32_fl, hid_fl = mlp_flops_per_particle(model, plan)
     f32_fl, hid_fl = f32_fl * B * S, hid_fl * B * S
     flops = f32_fl + hid_fl
@@ -347,6 +418,8 @@ def main():
     exps = kde_exps_per_particle(model, plan) * B * S
     traffic, traffic_src = load_traffic(args.config)
     kern_s = kern_ms * 1e-3
+    ex_f32, ex_hid, ex_exps = executed_work(model, plan, B, S, precomputed)
+    ex_flops = ex_f32 + ex_hid
     if exps > 0.1 * flops / 64:
         # KDE: one exp per (particle, point) kernel weight; the bound is the v_exp_f32 issue rate
         ach = exps / kern_s / 1e12
@@ -354,6 +427,8 @@ def main():
                 "frac": round(ach / EXP_PEAK_T, 4), "traffic": traffic, "kernel": kernel_name,
                 "kernel_ms": round(kern_ms, 4), "exps_per_launch": exps,
                 "peak_basis": "v_exp_f32 issue: 8 cyc per wave64 per SIMD, 1024 SIMDs, 2.4 GHz",
+                "executed_exps_per_launch": ex_exps,
+                "executed_frac": round(ex_exps / kern_s / 1e12 / EXP_PEAK_T, 4),
                 "launches_timed": reps, "launches_untimed_before": untimed + 1}
     else:
         # blended peak: each FLOP class at the dense peak of the unit that runs it
@@ -366,6 +441,9 @@ def main():
                 "hidden_layer": "f32 MFMA" if exact else "split-f16 MFMA (3 pass, f32 accumulate)",
                 "peak_basis": f"f32 FLOPs at {FP32_PEAK_TFLOPS} TF, hidden-layer FLOPs at {hid_peak:.1f} TF",
                 "f32_equiv_frac_of_fp32_peak": round(achieved / FP32_PEAK_TFLOPS, 4),
+                "executed_flops_per_launch": ex_flops,
+                "executed_frac": round(ex_flops / kern_s / 1e12 /
+                                       (ex_flops / (ex_f32 / (FP32_PEAK_TFLOPS * 1e12) + ex_hid / (hid_peak * 1e12)) / 1e12), 4),
                 "launches_timed": reps, "launches_untimed_before": untimed + 1}
     roof["traffic_source"] = traffic_src
 
@@ -391,12 +469,14 @@ def main():
                    "walk": ("plan-specialised (step table compiled in with hiprtc)" if specialised
                             else "step-table interpreter"),
                    "plan_compile_s": round(jit.STATS["compile_s"], 2), "plan_cache_hits": jit.STATS["disk_hits"],
-                   "first_call_s": round(t_first, 2),
+                   "first_call_s": round(t_first, 2), "background_compile_wait_s": round(t_wait, 2),
                    "shared_sample_precompute_nodes": n_precomp},
         "roofline": roof,
     }
     if fallbacks:
         out["config"]["is_fallback_steps"] = sum(fallbacks)
+    if gather_info is not None:
+        out["gather"] = gather_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         kde = "kde" in cfg["kinds"]
         nq = args.cpu_queries or (1024 if cfg["engine"] == "monte_carlo_marginalization" and cfg["n_nodes"] <= 64

@@ -27,6 +27,7 @@ def plans_for(name):
     """``cfg`` (the bench engine) or ``cfg:engine`` (mcm / is / lw / ancestral: the engines'
     plans for the GPU tests' workloads, which share the bench configs' DAGs)."""
     import bench
+    from vectorizedbayesiannetwork_amd import engines as E
     from vectorizedbayesiannetwork_amd import plan as P
     cfg_name, _, eng_name = name.partition(":")
     cfg, model, target, ev = bench.build_model(cfg_name)
@@ -38,13 +39,13 @@ def plans_for(name):
     if eng == "likelihood_weighting":
         plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[x for x in model.topo if x in vals],
                             out_nodes=[target], shared_roots=True, mode=P.MODE_WEIGHTED, skip=[])
-        pc = P.precompute_plans(pk, plan)
-        return cfg, [("plain", plan, False)] + ([("precompute", pc[0], True)] if pc else [])
+        pc = P.precompute_plans(pk, plan, per_query=E.PRECOMPUTE_Q)
+        return cfg, [("plain", plan, False)] + ([("precompute", pc[0], pc[1] is not None)] if pc else [])
     if eng == "ancestral":
         plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[], out_nodes=[target], shared_roots=True,
                             mode=P.MODE_SAMPLE, skip=[])
-        pc = P.precompute_plans(pk, plan)
-        return cfg, [("plain", plan, False)] + ([("precompute", pc[0], True)] if pc else [])
+        pc = P.precompute_plans(pk, plan, per_query=E.PRECOMPUTE_Q)
+        return cfg, [("plain", plan, False)] + ([("precompute", pc[0], pc[1] is not None)] if pc else [])
     if eng == "importance_sampling":
         plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[x for x in model.topo if x in vals],
                             out_nodes=[target], shared_roots=False, mode=P.MODE_WEIGHTED, skip=[])
@@ -54,26 +55,39 @@ def plans_for(name):
     else:
         return cfg, []
     out = [("plain", plan, False)]
-    pc = P.precompute_plans(pk, plan) if eng != "importance_sampling" else None
+    pc = P.precompute_plans(pk, plan, per_query=E.PRECOMPUTE_Q)
     if pc is not None:
-        out.append(("precompute", pc[0], True))
+        out.append(("precompute", pc[0], pc[1] is not None))
     return cfg, out
 
 
+def _one(name):
+    from vectorizedbayesiannetwork_amd import jit
+    cfg, plans = plans_for(name)
+    lines = []
+    for tag, plan, pre in plans:
+        t0 = time.perf_counter()
+        key, comp = jit.precompile(plan, cfg["B"], cfg["S"], precomp=pre)
+        lines.append(f"{name} {tag}: {key} ({'compiled' if comp else 'cached'} in {time.perf_counter() - t0:.1f} s)")
+    return lines
+
+
 def main(names):
-    from vectorizedbayesiannetwork_amd import jit, synthetic
+    from concurrent.futures import ProcessPoolExecutor
+    from vectorizedbayesiannetwork_amd import synthetic
     names = names or ["cfg2", "cfg3", "cfg4", "cfg5", "anchor64"]
     if names == ["--tests"]:                 # the extra plans of the GPU tests' workloads
-        names = ["cfg2:is", "cfg2:lw", "cfg3:lw", "cfg3:ancestral", "cfg5:ancestral"]
+        names = ["cfg2:is", "cfg2:lw", "cfg3:lw", "cfg3:mcm", "cfg3:ancestral", "cfg4:lw", "cfg4:ancestral",
+                 "cfg5:lw", "cfg5:ancestral"]
     for name in names:
         if name.partition(":")[0] not in synthetic.CONFIGS or name.partition(":")[2] not in ("", *ENGINES):
             raise SystemExit(f"unknown config {name}")
-        cfg, plans = plans_for(name)
-        for tag, plan, pre in plans:
-            t0 = time.perf_counter()
-            key, comp = jit.precompile(plan, cfg["B"], cfg["S"], precomp=pre)
-            print(f"{name} {tag}: {key} ({'compiled' if comp else 'cached'} in {time.perf_counter() - t0:.1f} s)",
-                  flush=True)
+    # one hiprtc compile per process at a time (single-threaded, ~1-2 GB each)
+    workers = max(1, min(len(names), (os.cpu_count() or 1), 8))
+    with ProcessPoolExecutor(workers) as ex:
+        for lines in ex.map(_one, names):
+            for ln in lines:
+                print(ln, flush=True)
 
 
 if __name__ == "__main__":

@@ -189,3 +189,59 @@ def test_slice_noise_forms():
         slice_noise(torch.randn(2, 2, B + 1, 3, 1), 0, 2, B)
     with pytest.raises(ValueError):
         slice_noise((w, torch.randn(3, B)), 0, 2, B)
+
+
+class SeededStub(StubEngine):
+    """A stub with the engines' own deterministic seed sequence (``seed`` set: seed + call)."""
+
+    def __init__(self, seed):
+        super().__init__()
+        self.seed = seed
+        self._calls = 0
+
+    def _seed(self, kwargs):
+        s = self.seed + self._calls
+        self._calls += 1
+        return s
+
+
+def _seeded_worker(rank, world, init, ev, out_q, calls):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    try:
+        torch.manual_seed(999 + rank)                 # irrelevant: the engine's own sequence rules
+        eng = ShardedEngine(SeededStub(4242), gather=True, overlap=True)
+        outs, pending = [], []
+        for _ in range(calls):
+            pdf, xs = eng.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}))
+            pending.append(len(eng._pending))
+            if pdf is not None:
+                eng.wait()
+                outs.append(pdf.clone())
+        out_q.put((rank, outs, pending, eng.gather_bytes))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_sharded_engine_keeps_a_seeded_engines_sequence():
+    """A wrapped engine with ``seed`` set keeps its own sequence (seed + call index) on every
+    rank, so sharded calls equal the unsharded engine's; non-destination ranks that never
+    wait() hold no unbounded list of finished gathers; rank 0 counts the bytes it receives."""
+    ev = torch.linspace(-1, 1, 8).unsqueeze(1)
+    calls = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = _rendezvous()
+    procs = [ctx.Process(target=_seeded_worker, args=(r, 2, init, ev, q, calls)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    (_, outs, _, nbytes), (_, outs1, pending1, _) = res
+    ref = SeededStub(4242)
+    for k in range(calls):
+        rpdf, _ = ref.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}), seed=ref._seed({}))
+        assert torch.equal(outs[k], rpdf)
+    assert outs1 == [] and max(pending1) <= 3, pending1
+    shard = 4 * S * 4 + 4 * S * 1 * 4                 # pdf [4, S] + samples [4, S, 1] fp32 from rank 1
+    assert nbytes == calls * shard

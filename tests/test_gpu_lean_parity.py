@@ -5,18 +5,21 @@ read a noise buffer.  The bench and every production call run the *lean* instant
 (no injected draws, no segment state: csrc ``vbn_walk.hip`` kind-set bit 7), which makes its
 own Philox draws and pairs Box-Muller normals across steps.  Here the oracle
 (oracle/vbn_oracle.py, the reference op sequence) is fed a host replica of exactly those
-draws (tests/philox_draws.py) and the two are compared per particle on the cfg2 and cfg3
-DAGs of SURVEY §8(d) (32 nodes, B = 8 queries x S = 1024 samples), for MCM, IS, LW and
-ancestral; then a full-size cfg2 launch is checked statistically against the oracle with
-the reference's own torch RNG.
+draws (tests/philox_draws.py) and the two are compared per particle on every DAG of SURVEY
+§8(d): cfg2 / cfg3 (32 nodes, B = 8 x S = 1024), cfg4 (64 KDE nodes with M = 10,000 points,
+B = 2 x S = 1024) and cfg5 (128 nodes, five families, KDE M = 4096, B = 1 x S = 2048, the
+config's own sample count), for MCM, IS, LW and ancestral, on the step-table interpreter and
+the plan-specialised kernel, with the shared-sample precompute on; then one full-size launch
+per config (cfg2, cfg4, cfg5) is checked statistically against the oracle with the
+reference's own torch RNG.
 
-Tolerances (as tests/test_gpu_parity.py): samples |d| <= 1e-4 + 1e-4 |x|; pdf |d| <= 1e-6 +
-2e-3 |pdf|; log-weights |d| <= 2e-3 (the pdf's relative bound in log space).  A categorical
-(mdn component / softmax_nn class) choice is made from fp32 probabilities on the GPU and from
-float64 ones on the host; a particle may differ only if one of its categorical uniforms lies
-within ``TIE`` (CDF units) of a class boundary, and the number of such particles is
-reported.  Reference: monte_carlo_marginalization.py:60-91, importance_sampling.py:37-93,
-likelihood_weighting.py:36-82, sampling/ancestral.py:13-41.
+Tolerances: samples |d| <= 1e-5 + 1e-5 |x|; pdf |d| <= 1e-4 |pdf| (log-density
+1e-4); log-weights |d| <= 1e-4.  A categorical (mdn component / softmax_nn class / KDE point)
+choice is made from fp32 probabilities on the GPU and from float64 ones on the host; a
+particle may differ only if one of its categorical uniforms lies within ``TIE`` (CDF units) of
+a class boundary, and the number of such particles is capped and reported.  Reference:
+monte_carlo_marginalization.py:60-91, importance_sampling.py:37-93,
+likelihood_weighting.py:36-82, sampling/ancestral.py:13-41, cpds/kde.py:151-182.
 """
 from __future__ import annotations
 
@@ -32,11 +35,12 @@ from workloads import synthetic_workload
 
 pytestmark = pytest.mark.gpu
 
-S_ATOL, S_RTOL = 1e-4, 1e-4
-P_ATOL, P_RTOL = 1e-6, 2e-3
-LW_ATOL = 2e-3
+S_ATOL, S_RTOL = 1e-5, 1e-5
+P_ATOL, P_RTOL = 1e-30, 1e-4
+LW_ATOL = 1e-4
 TIE = 1e-5                       # |u - CDF boundary| below which a class choice may flip
-B_PARITY, S_PARITY = 8, 1024
+# (B, S) of the per-particle comparisons: sizes the oracle finishes in seconds
+SIZES = {"cfg2": (8, 1024), "cfg3": (8, 1024), "cfg4": (2, 1024), "cfg5": (1, 2048)}
 
 
 def _workload(cfg_name: str, n_queries: int):
@@ -65,6 +69,13 @@ def _mismatch(got, ref, atol, rtol):
 
 
 def _check(name, bad, draws, n_expect):
+    """Every differing particle must carry a categorical near-tie, and few may differ: at most
+    0.1 % of the particles plus 1 % of the near-tie ones (at least 2).  A tie flips only when
+    the GPU's fp32 CDF error (~1e-6 of the total) exceeds its margin (< TIE = 1e-5), so most ties
+    do not flip; with M = 10,000 KDE points almost every particle of the KDE DAGs has some draw
+    within TIE of a point boundary (measured: cfg4 2 and 5 differing particles of 2048, all
+    near-ties; mdn / softmax_nn DAGs 0 of 8192), which is why the cap, not the tie mask, is the
+    KDE check."""
     ties = draws.min_margin() < TIE
     unexplained = bad & ~ties
     print(f"{name}: {int(bad.sum())} differing particles of {bad.size}, "
@@ -73,57 +84,86 @@ def _check(name, bad, draws, n_expect):
     assert not unexplained.any(), (
         f"{name}: {int(unexplained.sum())} particles differ without a categorical near-tie "
         f"(first at {np.argwhere(unexplained)[0].tolist()})")
-    assert bad.sum() <= max(2, bad.size // 1000), f"{name}: too many differing particles"
+    cap = max(2, bad.size // 1000 + int(ties.sum()) // 100)
+    assert bad.sum() <= cap, f"{name}: {int(bad.sum())} differing particles (cap {cap})"
 
 
-@pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3"])
-def test_lean_mcm_matches_oracle(cfg_name):
-    from vectorizedbayesiannetwork_amd import engines as E
-    from vectorizedbayesiannetwork_amd.engines import MonteCarloMarginalization, Query
-    model, vbn, target, ev = _workload(cfg_name, B_PARITY)
-    seed = 20260417
-    pdf, xs = MonteCarloMarginalization(n_samples=S_PARITY).infer_posterior(
-        vbn, Query(target, {k: v.cuda() for k, v in ev.items()}), seed=seed)
-    torch.cuda.synchronize()
+def _errors(got, ref, bad):
+    """max |d| over the particles that agree (the tolerance check above covers them)."""
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    ok = torch.from_numpy(~bad)
+    if got.dim() == 3:
+        ok = ok.unsqueeze(-1).expand_as(got)
+    fin = torch.isfinite(ref) & torch.isfinite(got) & ok
+    return float((got - ref).abs()[fin].max()) if fin.any() else 0.0
+
+
+def _q(target, ev):
+    from vectorizedbayesiannetwork_amd.engines import Query
+    return Query(target, {k: v.cuda() for k, v in ev.items()})
+
+
+def _lean_launch(plan_jit):
+    """the last launch was the production walk (lean: no injected draws, no segment state), in
+    the requested form, with the shared-sample precompute wherever the plan has one"""
+    from vectorizedbayesiannetwork_amd import engines as E, ops
     last = E.LAST_LAUNCH
     assert last["noise"] is None and last["state"] is None, "the production walk must be the lean one"
-    draws = _provider(last["plan"], last["pk"], seed, B_PARITY, S_PARITY)
-    rpdf, rxs = O.monte_carlo_marginalization(model, target, ev, {}, S_PARITY, draws)
-    bad_x, ex = _mismatch(xs, rxs, S_ATOL, S_RTOL)
-    bad_p, ep = _mismatch(pdf, rpdf, P_ATOL, P_RTOL)
-    print(f"{cfg_name} MCM max |dx| {ex:.3g}, max |dpdf| {ep:.3g}")
-    _check(f"{cfg_name} MCM", bad_x | bad_p, draws, (B_PARITY, S_PARITY))
+    assert last["precomputed"] == (last["plan"].pc is not None)
+    if plan_jit != "auto":
+        assert bool(ops.LAST_WALK.get("specialised")) == plan_jit
+    return last
 
 
 @pytest.mark.parametrize("plan_jit", [False, True])
-@pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3"])
-@pytest.mark.parametrize("engine", ["importance_sampling", "likelihood_weighting"])
+@pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3", "cfg4", "cfg5"])
+def test_lean_mcm_matches_oracle(cfg_name, plan_jit):
+    from vectorizedbayesiannetwork_amd.engines import MonteCarloMarginalization
+    b, s = SIZES[cfg_name]
+    model, vbn, target, ev = _workload(cfg_name, b)
+    seed = 20260417
+    pdf, xs = MonteCarloMarginalization(n_samples=s, plan_jit=plan_jit).infer_posterior(
+        vbn, _q(target, ev), seed=seed)
+    torch.cuda.synchronize()
+    last = _lean_launch(plan_jit)
+    draws = _provider(last["plan"], last["pk"], seed, b, s)
+    rpdf, rxs = O.monte_carlo_marginalization(model, target, ev, {}, s, draws)
+    bad_x, _ = _mismatch(xs, rxs, S_ATOL, S_RTOL)
+    bad_p, _ = _mismatch(pdf, rpdf, P_ATOL, P_RTOL)
+    bad = bad_x | bad_p
+    lerr = _errors(torch.log(pdf), torch.log(rpdf), bad)
+    print(f"{cfg_name} MCM max |dx| {_errors(xs, rxs, bad):.3g}, max |dlog pdf| {lerr:.3g}")
+    _check(f"{cfg_name} MCM", bad, draws, (b, s))
+
+
+@pytest.mark.parametrize("plan_jit", [False, True])
+@pytest.mark.parametrize("cfg_name,engine", [("cfg2", "importance_sampling"), ("cfg2", "likelihood_weighting"),
+                                             ("cfg3", "importance_sampling"), ("cfg3", "likelihood_weighting"),
+                                             ("cfg4", "likelihood_weighting"), ("cfg5", "likelihood_weighting")])
 def test_lean_weighted_walk_matches_oracle(cfg_name, engine, plan_jit):
     """IS (per-query root draws, raw evidence) and LW (shared roots, clamped evidence)
     log-weights and target samples per particle, before normalisation; step-table interpreter
-    and plan-specialised kernel (the latter pinned here directly: with split-f16 MFMA heads its
-    evidence log-weights are not bitwise the interpreter's, test_gpu_jit.py)."""
-    from vectorizedbayesiannetwork_amd import engines as E
-    from vectorizedbayesiannetwork_amd.engines import ImportanceSampling, LikelihoodWeighting, Query
-    model, vbn, target, ev = _workload(cfg_name, B_PARITY)
+    and plan-specialised kernel."""
+    from vectorizedbayesiannetwork_amd.engines import ImportanceSampling, LikelihoodWeighting
+    b, s = SIZES[cfg_name]
+    model, vbn, target, ev = _workload(cfg_name, b)
     seed = 77001
-    q = Query(target, {k: v.cuda() for k, v in ev.items()})
     is_ = engine == "importance_sampling"
     cls = ImportanceSampling if is_ else LikelihoodWeighting
-    eng = cls(n_samples=S_PARITY, plan_jit=plan_jit)
-    log_w, xs = eng._walk(vbn, q, S_PARITY, clamp=not is_, shared_roots=not is_,
+    eng = cls(n_samples=s, plan_jit=plan_jit)
+    log_w, xs = eng._walk(vbn, _q(target, ev), s, clamp=not is_, shared_roots=not is_,
                           kwargs={"_seed_value": seed})
     torch.cuda.synchronize()
-    from vectorizedbayesiannetwork_amd import ops
-    assert bool(ops.LAST_WALK.get("specialised")) == plan_jit
-    last = E.LAST_LAUNCH
-    assert last["noise"] is None and last["state"] is None
-    draws = _provider(last["plan"], last["pk"], seed, B_PARITY, S_PARITY)
-    parts, rlw, cols = O._walk_weighted(model, ev, {}, S_PARITY, draws, clamp=not is_, per_query=is_)
-    bad_x, ex = _mismatch(xs, parts[..., cols[target]], S_ATOL, S_RTOL)
-    bad_w, ew = _mismatch(log_w, rlw, LW_ATOL, 0.0)
-    print(f"{cfg_name} {engine} max |dx| {ex:.3g}, max |dlogw| {ew:.3g}")
-    _check(f"{cfg_name} {engine} walk", bad_x | bad_w, draws, (B_PARITY, S_PARITY))
+    last = _lean_launch(plan_jit)
+    draws = _provider(last["plan"], last["pk"], seed, b, s)
+    parts, rlw, cols = O._walk_weighted(model, ev, {}, s, draws, clamp=not is_, per_query=is_)
+    rxs = parts[..., cols[target]]
+    bad_x, _ = _mismatch(xs, rxs, S_ATOL, S_RTOL)
+    bad_w, _ = _mismatch(log_w, rlw, LW_ATOL, 0.0)
+    bad = bad_x | bad_w
+    print(f"{cfg_name} {engine} max |dx| {_errors(xs, rxs, bad):.3g}, max |dlogw| {_errors(log_w, rlw, bad):.3g}")
+    _check(f"{cfg_name} {engine} walk", bad, draws, (b, s))
 
 
 @pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3"])
@@ -131,43 +171,43 @@ def test_lean_is_engine_matches_oracle(cfg_name):
     """The whole IS call: walk + wave-reduced softmax / ESS + batch-global fallback decision;
     a query may differ only if one of its particles had a categorical near-tie."""
     from vectorizedbayesiannetwork_amd import engines as E
-    from vectorizedbayesiannetwork_amd.engines import ImportanceSampling, Query
-    model, vbn, target, ev = _workload(cfg_name, B_PARITY)
+    from vectorizedbayesiannetwork_amd.engines import ImportanceSampling
+    b, s = SIZES[cfg_name]
+    model, vbn, target, ev = _workload(cfg_name, b)
     seed = 5150
-    eng = ImportanceSampling(n_samples=S_PARITY)
-    w, xs = eng.infer_posterior(vbn, Query(target, {k: v.cuda() for k, v in ev.items()}), seed=seed)
+    eng = ImportanceSampling(n_samples=s)
+    w, xs = eng.infer_posterior(vbn, _q(target, ev), seed=seed)
     torch.cuda.synchronize()
     if eng._last_fallback:
         pytest.skip("the IS -> LW fallback fired on this workload (LW walk covered above)")
     last = E.LAST_LAUNCH
-    draws = _provider(last["plan"], last["pk"], seed, B_PARITY, S_PARITY)
-    rw, rxs, ress, rfb = O.importance_sampling(model, target, ev, {}, S_PARITY, draws)
+    draws = _provider(last["plan"], last["pk"], seed, b, s)
+    rw, rxs, ress, rfb = O.importance_sampling(model, target, ev, {}, s, draws)
     assert rfb is False
     tie_q = (draws.min_margin() < TIE).any(axis=1)
     bad_w, ew = _mismatch(w.cpu(), rw, P_ATOL, P_RTOL)
     bad_e, ee = _mismatch(eng._last_ess.cpu().view(-1, 1), ress.view(-1, 1), 1e-5, P_RTOL)
     bad_q = bad_w.any(axis=1) | bad_e[:, 0]
-    print(f"{cfg_name} IS engine: {int(bad_q.sum())} differing queries of {B_PARITY} "
+    print(f"{cfg_name} IS engine: {int(bad_q.sum())} differing queries of {b} "
           f"({int(tie_q.sum())} with a categorical near-tie), max |dw| {ew:.3g}, max |dESS| {ee:.3g}")
     assert not (bad_q & ~tie_q).any(), "a query differs without a categorical near-tie"
 
 
-@pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3"])
-def test_lean_ancestral_matches_oracle(cfg_name):
-    from vectorizedbayesiannetwork_amd import engines as E
-    from vectorizedbayesiannetwork_amd.engines import AncestralSampler, Query
-    model, vbn, target, ev = _workload(cfg_name, B_PARITY)
+@pytest.mark.parametrize("plan_jit", [False, True])
+@pytest.mark.parametrize("cfg_name", ["cfg2", "cfg3", "cfg4", "cfg5"])
+def test_lean_ancestral_matches_oracle(cfg_name, plan_jit):
+    from vectorizedbayesiannetwork_amd.engines import AncestralSampler
+    b, s = SIZES[cfg_name]
+    model, vbn, target, ev = _workload(cfg_name, b)
     seed = 31337
-    xs = AncestralSampler(n_samples=S_PARITY).sample(
-        vbn, Query(target, {k: v.cuda() for k, v in ev.items()}), S_PARITY, seed=seed)
+    xs = AncestralSampler(n_samples=s, plan_jit=plan_jit).sample(vbn, _q(target, ev), s, seed=seed)
     torch.cuda.synchronize()
-    last = E.LAST_LAUNCH
-    assert last["noise"] is None and last["state"] is None
-    draws = _provider(last["plan"], last["pk"], seed, B_PARITY, S_PARITY)
-    rxs = O.ancestral(model, target, ev, {}, S_PARITY, draws)
-    bad, ex = _mismatch(xs, rxs, S_ATOL, S_RTOL)
-    print(f"{cfg_name} ancestral max |dx| {ex:.3g}")
-    _check(f"{cfg_name} ancestral", bad, draws, (B_PARITY, S_PARITY))
+    last = _lean_launch(plan_jit)
+    draws = _provider(last["plan"], last["pk"], seed, b, s)
+    rxs = O.ancestral(model, target, ev, {}, s, draws)
+    bad, _ = _mismatch(xs, rxs, S_ATOL, S_RTOL)
+    print(f"{cfg_name} ancestral max |dx| {_errors(xs, rxs, bad):.3g}")
+    _check(f"{cfg_name} ancestral", bad, draws, (b, s))
 
 
 def _moments(x: torch.Tensor):
@@ -183,18 +223,23 @@ def _moments(x: torch.Tensor):
     return m, var.sqrt(), se_m, se_sd
 
 
-def test_lean_cfg2_full_size_statistics():
-    """cfg2 at its full size (4096 queries x 1024 samples, one lean launch) against the
-    oracle with the reference's own torch RNG on the first 16 queries: per query, the target
-    sample mean / std and the mean pdf agree within 5 Monte-Carlo standard errors."""
-    from vectorizedbayesiannetwork_amd.engines import MonteCarloMarginalization, Query
-    model, vbn, target, ev = _workload("cfg2", 4096)
-    pdf, xs = MonteCarloMarginalization(n_samples=1024).infer_posterior(
-        vbn, Query(target, {k: v.cuda() for k, v in ev.items()}), seed=99)
+@pytest.mark.parametrize("cfg_name,nq", [("cfg2", 16), ("cfg4", 4), ("cfg5", 2)])
+def test_lean_full_size_statistics(cfg_name, nq):
+    """Each MCM config at its full single-GPU size (cfg2 / cfg4: 4096 queries x 1024 samples,
+    cfg5: 8192 x 2048; one lean launch, the bench's form) against the oracle with the
+    reference's own torch RNG on the first ``nq`` queries: per query, the target sample mean /
+    std and the mean pdf agree within 5 Monte-Carlo standard errors."""
+    from vectorizedbayesiannetwork_amd import synthetic
+    from vectorizedbayesiannetwork_amd.engines import MonteCarloMarginalization
+    cfg = synthetic.CONFIGS[cfg_name]
+    b, s = cfg["B"], cfg["S"]
+    model, vbn, target, ev = _workload(cfg_name, b)
+    pdf, xs = MonteCarloMarginalization(n_samples=s).infer_posterior(vbn, _q(target, ev), seed=99)
     torch.cuda.synchronize()
-    nq = 16
+    _lean_launch("auto")
+    assert pdf.shape == (b, s) and torch.isfinite(pdf).all() and torch.isfinite(xs).all()
     torch.manual_seed(123)
-    rpdf, rxs = O.monte_carlo_marginalization(model, target, {k: v[:nq] for k, v in ev.items()}, {}, 1024,
+    rpdf, rxs = O.monte_carlo_marginalization(model, target, {k: v[:nq] for k, v in ev.items()}, {}, s,
                                               O.TorchDraws())
     g_m, g_sd, g_sem, g_sesd = _moments(xs[:nq, :, 0].cpu())
     r_m, r_sd, r_sem, r_sesd = _moments(rxs[:, :, 0])
@@ -203,9 +248,8 @@ def test_lean_cfg2_full_size_statistics():
     z_m = (g_m - r_m).abs() / (g_sem ** 2 + r_sem ** 2).sqrt()
     z_sd = (g_sd - r_sd).abs() / (g_sesd ** 2 + r_sesd ** 2).sqrt()
     z_p = (gp_m - rp_m).abs() / (gp_se ** 2 + rp_se ** 2).sqrt()
-    print(f"cfg2 full size: max z mean {float(z_m.max()):.2f}, std {float(z_sd.max()):.2f}, "
+    print(f"{cfg_name} full size ({b} x {s}): max z mean {float(z_m.max()):.2f}, std {float(z_sd.max()):.2f}, "
           f"pdf {float(z_p.max()):.2f}")
-    assert torch.isfinite(pdf).all() and torch.isfinite(xs).all()
     assert float(z_m.max()) < 5 and float(z_sd.max()) < 5 and float(z_p.max()) < 5
 
 
@@ -213,11 +257,11 @@ def test_lean_cfg3_is_statistics():
     """cfg3 (mdn + softmax_nn, importance sampling) at 64 queries: self-normalised posterior
     mean of the target per query within 5 standard errors (delta-method SE) of the oracle's
     with the reference's torch RNG; median ESS ratio within 10 %."""
-    from vectorizedbayesiannetwork_amd.engines import ImportanceSampling, Query
+    from vectorizedbayesiannetwork_amd.engines import ImportanceSampling
     nq = 64
     model, vbn, target, ev = _workload("cfg3", nq)
     eng = ImportanceSampling(n_samples=1024)
-    w, xs = eng.infer_posterior(vbn, Query(target, {k: v.cuda() for k, v in ev.items()}), seed=7)
+    w, xs = eng.infer_posterior(vbn, _q(target, ev), seed=7)
     torch.cuda.synchronize()
     torch.manual_seed(321)
     rw, rxs, ress, rfb = O.importance_sampling(model, target, ev, {}, 1024, O.TorchDraws())

@@ -1,12 +1,15 @@
 """HIP path vs the oracle on the golden fixtures (same recorded draws injected).
 
-Tolerances (fp32; the MLPs' sums are reassociated by MFMA/FMA vs the CPU sgemm):
-  samples / target values : |d| <= 1e-4 + 1e-4 |x|
-  pdf (MCM)               : |d| <= 1e-6 + 2e-3 |pdf|     (log-density abs error ~1e-4..1e-3)
-  IS/LW weights           : |d| <= 1e-6 + 2e-3 |w|
-  ESS                     : rel 2e-3
+Tolerances (fp32, the MLPs' sums are reassociated by MFMA/FMA vs the CPU sgemm):
+  samples / target values : |d| <= 1e-5 + 1e-5 |x|
+  pdf (MCM), CPD log-probs: log-density |d| <= 1e-4  (pdf: |d| <= 1e-4 |pdf|)
+  IS/LW weights           : |d| <= 1e-4 |w|  (+1e-30: weights that underflow to 0)
+  ESS                     : rel 1e-4
   softmax_nn bin indices  : bit-exact (checked through the bin-boundary log_prob cases)
   IS fallback decision    : identical
+Categorical near-ties (large-M KDE fixtures: a recorded point whose CDF interval is narrower
+than WIDTH_TIE) are compared like every other particle; a particle outside tolerance must be
+one of them, and at most TIE_CAP of them may differ (counted and printed per case).
 All run through the C-ABI library (vbn_hip_walk / vbn_hip_normalize_weights).
 """
 import math
@@ -20,11 +23,13 @@ from oracle import vbn_oracle as O
 
 pytestmark = pytest.mark.gpu
 
-S_ATOL, S_RTOL = 1e-4, 1e-4
-P_ATOL, P_RTOL = 1e-6, 2e-3
+S_ATOL, S_RTOL = 1e-5, 1e-5
+P_ATOL, P_RTOL = 1e-30, 1e-4
+LP_ATOL, LP_RTOL = 1e-4, 0.0
 # large-M KDE fixtures (make_golden_large.py): a point whose CDF interval is narrower than this
 # (fp32 chunk sums over up to 640 points vs the reference's float64 interval) may flip
 WIDTH_TIE = 2e-5
+TIE_CAP = 0.5          # at most this fraction of the near-tie particles may differ
 
 
 def _vbn(fx):
@@ -34,25 +39,34 @@ def _vbn(fx):
     return model, VBN.from_model(model, device="cuda")
 
 
-def _close(name, got, ref, atol, rtol, allow=None):
-    """``allow`` [B, S]: particles exempt from the comparison (categorical near-ties)."""
+def _close(name, got, ref, atol, rtol, ties=None):
+    """Elementwise |got - ref| <= atol + rtol |ref| with identical NaN / +-inf patterns.
+    ``ties`` [B|1, S]: particles with a categorical near-tie; a particle may be out of tolerance
+    only if it is one of them, and at most TIE_CAP of them (at least one) may be."""
     got = got.detach().float().cpu()
     ref = ref.detach().float().cpu()
     assert got.shape == ref.shape, f"{name}: shape {tuple(got.shape)} vs {tuple(ref.shape)}"
-    if allow is not None and allow.any() and got.dim() >= 2 and got.shape[1] == allow.shape[1]:
-        a = allow if allow.shape[0] == got.shape[0] else allow.any(0, keepdim=True).expand(got.shape[0], -1)
-        a = a.view(a.shape + (1,) * (got.dim() - 2)).expand_as(got)
-        got, ref = torch.where(a, ref, got), ref
     nan_g, nan_r = torch.isnan(got), torch.isnan(ref)
-    assert torch.equal(nan_g, nan_r), f"{name}: NaN pattern differs"
-    inf_ok = torch.equal(torch.isinf(got) & (got > 0), torch.isinf(ref) & (ref > 0)) and \
-        torch.equal(torch.isinf(got) & (got < 0), torch.isinf(ref) & (ref < 0))
-    assert inf_ok, f"{name}: inf pattern differs"
-    m = ~(nan_g | torch.isinf(ref))
-    err = (got[m] - ref[m]).abs()
-    tol = atol + rtol * ref[m].abs()
-    bad = (err > tol)
-    assert not bad.any(), f"{name}: {int(bad.sum())} of {err.numel()} out of tolerance, max err {float(err.max()):.3g}"
+    pos_g, pos_r = torch.isinf(got) & (got > 0), torch.isinf(ref) & (ref > 0)
+    neg_g, neg_r = torch.isinf(got) & (got < 0), torch.isinf(ref) & (ref < 0)
+    fin = torch.isfinite(got) & torch.isfinite(ref)
+    err = torch.where(fin, (got - ref).abs(), torch.zeros_like(got))
+    bad = (nan_g != nan_r) | (pos_g != pos_r) | (neg_g != neg_r) | (fin & (err > atol + rtol * ref.abs()))
+    n_tie = n_bad = 0
+    if ties is not None and ties.any() and got.dim() >= 2 and got.shape[1] == ties.shape[1]:
+        t = ties if ties.shape[0] == got.shape[0] else ties.any(0, keepdim=True).expand(got.shape[0], -1)
+        pb = bad.reshape(got.shape[0], got.shape[1], -1).any(-1)          # per particle
+        n_tie, n_bad = int(t.sum()), int(pb.sum())
+        unexplained = pb & ~t
+        assert not unexplained.any(), (f"{name}: {int(unexplained.sum())} particles out of tolerance without a "
+                                       f"categorical near-tie, max err {float(err[bad].max()):.3g}")
+        assert n_bad <= max(1, int(TIE_CAP * n_tie)), f"{name}: {n_bad} of {n_tie} near-tie particles differ"
+        keep = ~pb.view(pb.shape + (1,) * (got.dim() - 2)).expand_as(got)
+        emax = float(err[keep].max()) if keep.any() else 0.0
+        print(f"{name}: {n_bad} of {n_tie} near-tie particles differ; max err elsewhere {emax:.3g}")
+        return emax
+    assert not bad.any(), (f"{name}: {int(bad.sum())} of {bad.numel()} out of tolerance, "
+                           f"max err {float(err[bad].max()):.3g} (atol {atol}, rtol {rtol})")
     return float(err.max()) if err.numel() else 0.0
 
 
@@ -89,10 +103,10 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
         tm = tie_mask(case, model, 1 if par is None else par.shape[0], n, WIDTH_TIE)
         _close("cpd.sample", xs, ref, S_ATOL, S_RTOL, tm)
         lp = C.cpd_log_prob(vbn, node, ref.cuda(), None if par is None else par.cuda())
-        _close("cpd.log_prob(sampled)", lp, O.cpd_log_prob(rec, ref, par), 2e-4, 1e-4)
+        _close("cpd.log_prob(sampled)", lp, O.cpd_log_prob(rec, ref, par), LP_ATOL, LP_RTOL)
         if "x" in case:
             lpx = C.cpd_log_prob(vbn, node, case["x"].cuda(), None if par is None else par.cuda())
-            _close("cpd.log_prob(x)", lpx, O.cpd_log_prob(rec, case["x"], par), 2e-4, 1e-4)
+            _close("cpd.log_prob(x)", lpx, O.cpd_log_prob(rec, case["x"], par), LP_ATOL, LP_RTOL)
         return
     if eng == "conditional":                  # CPDHandle.conditional (cpd_handle.py:348-404)
         node = case["node"]
@@ -112,14 +126,14 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
         out = C.cpd_forward(vbn, node, None if par is None else par.cuda(), n, _noise=nd0)
         ref = O.cpd_forward(model.cpds[node], par, n, O.ReplayDraws(case["draws"]))
         _close("forward.samples", out.samples, ref["samples"], S_ATOL, S_RTOL)
-        _close("forward.log_prob", out.log_prob, ref["log_prob"], 2e-4, 1e-4)
+        _close("forward.log_prob", out.log_prob, ref["log_prob"], LP_ATOL, LP_RTOL)
         _close("forward.pdf", out.pdf, ref["pdf"], P_ATOL, P_RTOL)
         return
     if eng == "posterior_stats":
         st = vbn._posterior_stats(case["pdf"].cuda(), case["samples_in"].cuda())
         ref = O.posterior_stats(case["pdf"], case["samples_in"])
         for k in ("mean", "std", "ess"):
-            _close(k, st[k], ref[k], 1e-5, 1e-4)
+            _close(k, st[k], ref[k], 1e-5, 1e-5)
         return
     q = case["query"]
     qq = vbn._normalize_query(q)
@@ -128,7 +142,7 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
     nb = int(next(iter((q["evidence"] or q["do"]).values())).shape[0]) if (q["evidence"] or q["do"]) else 1
     tm = tie_mask(case, model, nb, n, WIDTH_TIE)
     if tm is not None and tm.any():
-        print(f"{name}[{idx}]: {int(tm.sum())} particles with a categorical near-tie (< {WIDTH_TIE}) exempt")
+        print(f"{name}[{idx}]: {int(tm.sum())} particles with a categorical near-tie (< {WIDTH_TIE})")
     if eng == "monte_carlo_marginalization":
         pdf, xs = MonteCarloMarginalization(n_samples=n, kde_valu=kde_valu).infer_posterior(vbn, qq, _noise=nd0)
         rpdf, rxs = O.monte_carlo_marginalization(model, q["target"], q["evidence"], q["do"], n, draws)
@@ -148,7 +162,7 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
         rw, rxs, ress, rfb = O.importance_sampling(model, q["target"], q["evidence"], q["do"], n, draws,
                                                    ess_threshold=e.ess_threshold)
         assert e._last_fallback == rfb == case["outputs"]["fallback"]
-        _close("ess", e._last_ess, ress, 1e-5, P_RTOL)
+        _close("ess", e._last_ess, ress, 1e-5, 1e-4)
         _close("samples", xs, rxs, S_ATOL, S_RTOL, tm)
         _close("weights", w, rw, P_ATOL, P_RTOL, tm)
     elif eng == "ancestral":
@@ -164,7 +178,7 @@ def test_golden_case_on_gpu(name, idx, kde_valu):
             resample=p.get("resample", True), clamp_obs=p.get("clamp_obs", True))
         assert e._last_resampled == rrs == case["outputs"]["resampled"]
         if ress is not None:
-            _close("ess", e._last_ess, ress, 1e-5, P_RTOL)
+            _close("ess", e._last_ess, ress, 1e-5, 1e-4)
         _close("samples", xs, rxs, S_ATOL, S_RTOL)
         _close("weights", w, rw, P_ATOL, P_RTOL)
     elif eng == "rao_blackwellized_marginalization":
@@ -221,7 +235,7 @@ def test_softmax_bins_bit_exact_on_gpu():
             ref = O.cpd_log_prob(rec, xs, par)
             assert torch.equal(torch.isinf(got), torch.isinf(ref)), (name, node)
             fin = torch.isfinite(ref)
-            assert torch.allclose(got[fin], ref[fin], atol=2e-4, rtol=1e-4), (name, node)
+            assert torch.allclose(got[fin], ref[fin], atol=LP_ATOL, rtol=0.0), (name, node)
             bins = O.smx_x_to_bin(rec, xs.unsqueeze(1))
             assert int(bins.min()) >= 0 and int(bins.max()) <= int(rec.hp("n_classes")) - 1
             seen += 1

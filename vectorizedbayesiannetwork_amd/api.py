@@ -256,6 +256,90 @@ class VBN:
             return {k: v.detach() for k, v in out.items()}
         return out.detach()
 
+    def precompile(self, signatures, *, n_samples: Optional[int] = None, background: bool = False) -> Dict[str, int]:
+        """Compile the plan-specialised walks (jit.py) of query signatures ahead of time, so no
+        later ``infer_posterior`` / ``sample`` call of those signatures runs the interpreter or
+        waits for hiprtc.  ``signatures``: iterable of dicts ``{"target": name, "evidence": names,
+        "do": names}`` (names as a list or the keys of a dict; the benchmark adapter's batches
+        share one signature per evidence skeleton, benchmarking/models/vbn.py:678-693).  The
+        configured inference method (and, when set, the sampling method: ancestral only) builds
+        each plan exactly as a call would; nothing is launched.  ``background``: start the
+        compiles on background threads and return at once (jit.wait_pending() joins).
+        Returns {"plans": n, "ready": n already loadable}."""
+        from . import engines as E
+        out = {"plans": 0, "ready": 0}
+        methods = []
+        if self._inference is not None:
+            methods.append("infer")
+        if self._sampling is not None and type(self._sampling).__name__ == "AncestralSampler":
+            methods.append("sample")
+        if not methods:
+            raise RuntimeError("Call set_inference_method(...) or set_sampling_method(...) before precompile().")
+        for sig in signatures:
+            names = {k: list(sig.get(k) or []) for k in ("evidence", "do")}
+            q = {"target": sig.get("target") or sig.get("target_feature"),
+                 "evidence": {n: torch.zeros(1, self.model.out_dim(n)) for n in names["evidence"]},
+                 "do": {n: torch.zeros(1, self.model.out_dim(n)) for n in names["do"]}}
+            kw = {} if n_samples is None else {"n_samples": int(n_samples)}
+            with E.precompile_mode("background" if background else "sync") as st:
+                if "infer" in methods:
+                    self.infer_posterior(q, **kw)
+                if "sample" in methods:
+                    self.sample(q, **({} if n_samples is None else {"n_samples": int(n_samples)}))
+            out["plans"] += st["plans"]
+            out["ready"] += st["ready"]
+        return out
+
+    def pack_query(self, signature, method: str = "monte_carlo_marginalization", *, n_samples: int = 1024,
+                   **method_kwargs) -> Dict[str, Any]:
+        """The packed plan of one query signature for the query-level custom ops
+        (``torch.ops.vbn_hip.mcm`` / ``is_lw`` / ``ancestral``, ops.py): the walk the engine
+        ``method`` would launch, with its precompute variant and pre-passes.  Returns
+        {"plan": int32 host tensor (vbn_hip::pack_plan), "params": the device parameter blob,
+        "fixed_nodes": evidence / do node names in the order of the ``fixed`` [B, fixed_ld]
+        buffer's columns, "fixed_cols": their first columns, "out_nodes": the output nodes,
+        "op": the op to call}.  ``signature``: {"target": name, "evidence": names, "do": names}."""
+        from . import engines as E
+        from . import ops
+        from .registry import INFERENCE_REGISTRY, SAMPLING_REGISTRY
+        ops_of = {"monte_carlo_marginalization": "mcm", "importance_sampling": "is_lw",
+                  "likelihood_weighting": "is_lw", "ancestral": "ancestral"}
+        if method not in ops_of:
+            raise ValueError(f"pack_query: method must be one of {sorted(ops_of)}")
+        names = {k: list(signature.get(k) or []) for k in ("evidence", "do")}
+        q = self._normalize_query({"target": signature.get("target"),
+                                   "evidence": {n: torch.zeros(1, self.model.out_dim(n)) for n in names["evidence"]},
+                                   "do": {n: torch.zeros(1, self.model.out_dim(n)) for n in names["do"]}})
+        with E.precompile_mode("none") as st:
+            if method == "ancestral":
+                SAMPLING_REGISTRY[method](n_samples=n_samples, **method_kwargs).sample(self, q, n_samples)
+            else:
+                INFERENCE_REGISTRY[method](n_samples=n_samples, **method_kwargs).infer_posterior(self, q)
+        seen = st["seen"]
+        if not seen:
+            raise RuntimeError("pack_query: the engine launched no walk for this signature")
+        plan = seen[0]
+        pk = E.packed_model(self, E._device_of(self))
+        secs = [plan, plan.pc, plan.pre, plan.pre_q]
+        empty = torch.zeros(0, dtype=torch.int32)
+        steps, ics, ocs, meta = [], [], [], []
+        for p in secs:
+            if p is None:
+                steps.append(empty), ics.append(empty), ocs.append(empty)
+                meta += [0] * 8
+                continue
+            steps.append(torch.from_numpy(p.steps._vbn_host[0]))
+            ics.append(torch.from_numpy(p.steps._vbn_host[1]))
+            ocs.append(p.out_cols.cpu())
+            meta += [p.n_slots, p.max_out, p.fixed_ld, p.mode, p.kind_mask, p.wbuf, pk.dmax, len(p.noise_nodes)]
+        cols, c = [], 0
+        for n in plan.fixed_nodes:
+            cols.append(c)
+            c += self.model.out_dim(n)
+        return {"plan": ops.pack_plan(steps, ics, ocs, meta), "params": pk.params,
+                "fixed_nodes": list(plan.fixed_nodes), "fixed_cols": cols, "out_nodes": list(plan.out_nodes),
+                "op": ops_of[method]}
+
     # ---- posterior summaries (vbn.py:483-568) ---------------------------------------------
     def _posterior_stats(self, pdf: torch.Tensor, samples: torch.Tensor, *, eps: float = 1e-12
                          ) -> Dict[str, torch.Tensor]:

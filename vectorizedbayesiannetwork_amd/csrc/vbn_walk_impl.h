@@ -306,17 +306,22 @@ __device__ __forceinline__ f32x16 layer2_init(const vbn_step& st, const Lane& L,
   return b;
 }
 
-// y - f32(half h of packed f16 pair hp), exact: one v_fma_mix_f32 (reads the f16 in place).
-// Operands are VALU results (activation / cvt), never raw MFMA results, so no MFMA read hazard.
-__device__ __forceinline__ float sub_f16_lo(float y, uint32_t hp) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(y));
-  return r;
+// y - f32(half h of packed f16 pair ph), exact: one v_fma_mix_f32 (reads the f16 in place),
+// selected by the compiler from fma(f32(h), m, y) with m = -1 held opaque in an SGPR (a literal
+// -1 folds the fma into a subtraction, which gfx950 selects as cvt + sub).  Not inline asm: an
+// asm v_fma_mix is invisible to the hazard recognizer, which then does not pad its VGPR write
+// against an in-flight MFMA reading or writing that register -- the cause of round 3's
+// hipcc / hiprtc divergence of the split-f16 heads (the two compiles scheduled it differently).
+__device__ __forceinline__ float neg_one_sgpr() {
+  float m = -1.0f;
+  asm("" : "+s"(m));     // not volatile: CSE'd / hoisted like any pure value
+  return m;
 }
-__device__ __forceinline__ float sub_f16_hi(float y, uint32_t hp) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(y));
-  return r;
+__device__ __forceinline__ float sub_f16_lo(float y, f16x2 ph) {
+  return __builtin_fmaf((float)ph[0], neg_one_sgpr(), y);
+}
+__device__ __forceinline__ float sub_f16_hi(float y, f16x2 ph) {
+  return __builtin_fmaf((float)ph[1], neg_one_sgpr(), y);
 }
 
 // Layer 2 of one group on the split-f16 path from the activations y (|y| <= 32768 checked by
@@ -336,11 +341,10 @@ __device__ __forceinline__ f32x16 layer2_split(const uint4 (&w2h)[4], const f32x
     for (int j = 0; j < 8; j += 2) {
       const float y0 = y[8 * s2 + j], y1 = y[8 * s2 + j + 1];
       const f16x2 ph = __builtin_convertvector((f32x2){y0, y1}, f16x2);
-      const uint32_t hp = __builtin_bit_cast(uint32_t, ph);
 #ifdef VBN_ABL_NOSPLIT
       const f16x2 pl = ph;
 #else
-      const f16x2 pl = __builtin_convertvector((f32x2){sub_f16_lo(y0, hp), sub_f16_hi(y1, hp)}, f16x2);
+      const f16x2 pl = __builtin_convertvector((f32x2){sub_f16_lo(y0, ph), sub_f16_hi(y1, ph)}, f16x2);
 #endif
       bh[s2][j] = ph[0];
       bh[s2][j + 1] = ph[1];

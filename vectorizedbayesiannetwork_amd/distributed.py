@@ -101,6 +101,7 @@ class ShardedEngine:
         self._gen: Optional[torch.Generator] = None
         self._pending = []
         self.last_seed: Optional[int] = None
+        self.gather_bytes = 0           # bytes dst received from its peers over all calls (bench.py)
 
     def _device(self):
         backend = dist.get_backend(self.group) if dist.is_initialized() else "gloo"
@@ -109,8 +110,15 @@ class ShardedEngine:
         return torch.device("cpu")
 
     def _shared_seed(self, kwargs) -> int:
+        """The call's seed, identical on every rank without a per-call collective: an explicit
+        ``seed=``; else a wrapped engine's own deterministic sequence (``engine.seed`` set: seed +
+        call index, as the unsharded engine would use); else the rank-replicated stream, seeded
+        once from rank 0's torch generator (so ``torch.manual_seed`` before the FIRST call fixes
+        every later call's seed; later reseeding does not change the stream)."""
         if kwargs.get("seed") is not None:
             return int(kwargs["seed"])
+        if getattr(self.engine, "seed", None) is not None and hasattr(self.engine, "_seed"):
+            return int(self.engine._seed({}))
         if self._gen is None:                        # once: rank 0's draw, broadcast
             rank, world = _world(self.group)
             s = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
@@ -162,7 +170,11 @@ class ShardedEngine:
             out = torch.empty((world, q_max) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
             parts = list(out.unbind(0))
         work = dist.gather(src, parts, dst=self.dst, group=self.group, async_op=self.overlap)
+        if rank == self.dst:
+            self.gather_bytes += (world - 1) * src.numel() * src.element_size()   # received from peers
         if self.overlap:
+            # callers that never wait() (non-dst ranks) must not pile up finished Works
+            self._pending = [w for w in self._pending if not w.is_completed()]
             self._pending.append(work)
         if rank != self.dst:
             return None

@@ -33,6 +33,8 @@ For parity tests the draws can be injected (``_noise=``).
 """
 from __future__ import annotations
 
+import contextlib
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -114,19 +116,22 @@ def _plan(pk: PackedModel, key, **kw) -> QueryPlan:
     p = pk.model._cache.get(ck)
     if p is None:
         p = build_plan(pk, **kw)
-        if kw.get("shared_roots") and not kw.get("params"):
-            # shared root draws: nodes whose parents are all roots are computed once per sample
+        if not kw.get("params"):
+            # nodes whose parents are all shared root draws (once per sample) or all evidence
+            # (once per query)
             pc = precompute_plans(pk, p, skip=kw.get("skip", ()), exact_f32=kw.get("exact_f32", False),
-                                  kde_valu=kw.get("kde_valu", False))
+                                  kde_valu=kw.get("kde_valu", False), per_query=PRECOMPUTE_Q)
             if pc is not None:
-                p.pc, p.pre = pc
+                p.pc, p.pre, p.pre_q = pc
         pk.model._cache[ck] = p
     return p
 
 
-# shared-sample precompute (plan.precompute_plans) in production walks; False: every node per
-# particle (A/B, tests)
+# per-sample / per-query precompute (plan.precompute_plans) in production walks; False: every
+# node per particle (A/B, tests).  PRECOMPUTE_Q (env VBN_PRECOMP_Q=0: off) applies to plans
+# built afterwards
 PRECOMPUTE = True
+PRECOMPUTE_Q = os.environ.get("VBN_PRECOMP_Q", "1") != "0"
 
 
 def _fixed_values(query, device, clamp: bool = False) -> Dict[str, torch.Tensor]:
@@ -177,6 +182,26 @@ def _next_seed() -> int:
 # last walk launched (introspection for bench.py's per-kernel timing)
 LAST_LAUNCH: Dict[str, object] = {}
 
+# VBN.precompile: engines build their plans and compile the specialised walks without launching
+_PRECOMPILE: Dict[str, object] = {"on": False, "compile": "sync", "plans": 0, "ready": 0}
+
+
+@contextlib.contextmanager
+def precompile_mode(compile: str = "sync"):
+    """Inside, run_walk compiles (``compile`` "sync" or "background", jit.module_for; "none":
+    nothing) the walk each engine call would launch, records its plan and returns zero outputs
+    instead of launching it.  Yields a dict that holds, after the block, "plans" (walks seen),
+    "ready" (their specialised modules loaded) and "seen" (the plans)."""
+    prev = dict(_PRECOMPILE)
+    res: Dict[str, object] = {}
+    _PRECOMPILE.update(on=True, compile=compile, plans=0, ready=0, seen=[])
+    try:
+        yield res
+    finally:
+        res.update(plans=_PRECOMPILE["plans"], ready=_PRECOMPILE["ready"], seen=list(_PRECOMPILE["seen"]))
+        _PRECOMPILE.clear()
+        _PRECOMPILE.update(prev)
+
 
 def noise_tensor(pk: PackedModel, plan: QueryPlan, noise: Dict[str, Tuple], b: int, n: int) -> torch.Tensor:
     """Injected draws by node name -> kernel layout [n_latent, 2, b, n, Dmax].
@@ -216,26 +241,50 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
         noise_b = int(noise.shape[2])
         if noise.shape[3] != n or noise.shape[4] != pk.dmax:
             raise ValueError(f"noise must be [n_latent, 2, B|1, {n}, {pk.dmax}]")
-    precomp = None
+    precomp = precomp_q = None
     walk_plan = plan
-    if (PRECOMPUTE and plan.pc is not None and noise is None and state is None and step_begin == 0
-            and step_end < 0 and n % 64 == 0 and not fixed_per_particle):
+    pre_ran = False
+    use_pc = (PRECOMPUTE and plan.pc is not None and noise is None and state is None and step_begin == 0
+              and step_end < 0 and n % 64 == 0 and not fixed_per_particle)
+    if _PRECOMPILE["on"]:
+        # VBN.precompile / pack_query: compile (or load) the specialised walk this launch would
+        # run, record its plan, no launch
+        _PRECOMPILE.setdefault("seen", []).append(plan)
+        if state is None and noise is None and plan_jit and _PRECOMPILE["compile"] != "none":
+            from . import jit
+            wp = plan.pc if use_pc else plan
+            km = jit.walk_kind_set(wp, b, n, precomp=use_pc and plan.pre is not None)
+            host = wp.steps._vbn_host
+            dev = pk.device.index if pk.device.index is not None else 0
+            if jit.module_for(host[0], host[1], km, dev, host[2], compile=_PRECOMPILE["compile"]) is not None:
+                _PRECOMPILE["ready"] += 1
+            _PRECOMPILE["plans"] += 1
+        lp = torch.zeros(b, n, device=pk.device) if plan.mode != MODE_SAMPLE else torch.empty(0, device=pk.device)
+        return lp, torch.zeros(b, n, n_out_cols, device=pk.device)
+    if use_pc:
         # the per-sample quantities of nodes with shared-root parents, once per sample (same
-        # seed / offset: the pre-pass draws the main walk's root values), then the main walk
-        _, precomp = run_walk(pk, plan.pre, fixed, 1, n, seed=seed, offset=offset, plan_jit=0)
-        precomp = precomp.view(n, -1)
+        # seed / offset: the pre-pass draws the main walk's root values), the per-query ones of
+        # nodes with evidence parents, once per query (one wave of identical lanes), then the
+        # main walk
+        if plan.pre is not None:
+            _, precomp = run_walk(pk, plan.pre, fixed, 1, n, seed=seed, offset=offset, plan_jit=0)
+            precomp = precomp.view(n, -1)
+        if plan.pre_q is not None:
+            _, pq = run_walk(pk, plan.pre_q, fixed, b, 64, seed=seed, offset=offset, q_base=q_base, plan_jit=0)
+            precomp_q = pq.view(b, 64, -1)[:, 0].contiguous()
         walk_plan = plan.pc
-    # (the plan as given: a re-run of this launch repeats the pre-pass)
+        pre_ran = True
+    # (the plan as given: a re-run of this launch repeats the pre-passes)
     LAST_LAUNCH.update(pk=pk, plan=plan, fixed=fixed, b=b, n=n, fixed_per_particle=fixed_per_particle,
                        noise=noise, state=state, seed=seed, offset=offset, plan_jit=plan_jit,
-                       precomputed=precomp is not None)
+                       precomputed=pre_ran, q_base=q_base)
     plan = walk_plan
     args = (plan.steps, plan.in_cols, pk.params, fixed, noise, plan.out_cols, b, n,
             plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
             len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
             plan.mode != MODE_SAMPLE, plan.kind_mask)
     if state is None:
-        lp, x = ops.walk(*args, plan.wbuf, plan_jit, precomp)
+        lp, x = ops.walk(*args, plan.wbuf, plan_jit, precomp, precomp_q)
     else:
         lp, x = ops.walk_segment(*args, state, state_flags, step_begin, step_end, plan.wbuf)
     if plan.mode != MODE_SAMPLE:

@@ -9,13 +9,17 @@ launches it with the same arguments, grid and LDS as the interpreter
 (``vbn_hip_walk_module``): same device functions, same operation order, bit-identical
 outputs, no per-step loads or dispatch (cfg2 walk 1.01 -> 0.88 ms, cfg3 3.83 -> 3.05 ms).
 
-Compiled code objects are cached per process and on disk (``$VBN_HIP_CACHE``, default the
-package's ``plan_cache/``, which ``scripts/precompile_plans.py`` fills on the build host for the
-benchmark workloads), keyed by the source, the options, the hiprtc version and the headers.  Only lean
-full-wave walks are specialised (production MCM / IS / LW / ancestral); by default only
-launches of at least ``JIT_MIN_PARTICLES`` particles (a compile takes seconds) --
-``VBN_PLAN_JIT=0`` disables it, the engines' ``plan_jit=True`` forces it.  Without hiprtc, or
-when a compile fails, the interpreter runs (a warning is printed once).
+Compiled code objects are cached per process and on disk (``$VBN_HIP_CACHE``, the package's
+``plan_cache/`` -- which ``scripts/precompile_plans.py`` fills on the build host for the
+benchmark workloads -- and a per-user fallback for read-only installs), keyed by the source, the
+options, the hiprtc version and the headers.  In the engines' default ("auto") mode a launch
+runs the specialised walk whenever its code object is at hand; a launch of at least
+``JIT_MIN_PARTICLES`` particles whose plan is not compiled yet starts the compile on a
+background thread and runs the interpreter meanwhile (same outputs, bit for bit), so a new
+query signature never waits for hiprtc (12-50 s); :func:`wait_pending` joins the compiles and
+``VBN.precompile`` compiles a list of signatures ahead of time.  ``VBN_PLAN_JIT=0`` disables
+specialisation, the engines' ``plan_jit=True`` forces it (compiling in the call).  Without
+hiprtc, or when a compile fails, the interpreter runs (a warning is printed once).
 """
 from __future__ import annotations
 
@@ -40,11 +44,15 @@ OPTIONS = ("--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast-hon
            "-fno-slp-vectorize", "-fno-vectorize")
 
 _lock = threading.Lock()
+_stats_lock = threading.Lock()
+_bg_slots = threading.BoundedSemaphore(2)       # background hiprtc compiles at a time
 _modules: Dict[Tuple[int, str], int] = {}        # (device, key) -> module handle
+_codes: Dict[str, bytes] = {}                    # source key -> code object (this process)
+_jobs: Dict[str, "_Job"] = {}                    # source key -> background compile
 _failed: Dict[str, str] = {}
 _rtc = None
 _warned = False
-STATS = {"compiled": 0, "compile_s": 0.0, "disk_hits": 0, "loaded": 0}
+STATS = {"compiled": 0, "compile_s": 0.0, "disk_hits": 0, "loaded": 0, "background": 0}
 
 
 def enabled() -> bool:
@@ -136,15 +144,36 @@ def compile_source(src: str) -> bytes:
         rtc.hiprtcDestroyProgram(ctypes.byref(prog))
 
 
+PACKAGE_CACHE = os.path.join(HERE, "plan_cache")
+
+
+def _read_dirs():
+    """Directories searched for a compiled plan: $VBN_HIP_CACHE, then the package's plan_cache
+    (code objects precompiled on the build host by scripts/precompile_plans.py travel with the
+    built library), then the per-user fallback -- whether or not they are writable."""
+    out = []
+    for d in (os.environ.get("VBN_HIP_CACHE"), PACKAGE_CACHE, _user_cache()):
+        if d and d not in out:
+            out.append(d)
+    return out
+
+
+def _user_cache() -> str:
+    base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
+    return os.path.join(base, "vbn_hip_plans")
+
+
 def _cache_dir() -> Optional[str]:
-    # default: in the package tree, so code objects precompiled on the build host
-    # (scripts/precompile_plans.py, __graft_entry__.build) travel with the built library
-    d = os.environ.get("VBN_HIP_CACHE") or os.path.join(HERE, "plan_cache")
-    try:
-        os.makedirs(d, exist_ok=True)
-        return d if os.access(d, os.W_OK) else None
-    except OSError:
-        return None
+    """First writable directory for new code objects: $VBN_HIP_CACHE or the package's
+    plan_cache, else the per-user fallback (read-only installs), else None (not persisted)."""
+    for d in (os.environ.get("VBN_HIP_CACHE") or PACKAGE_CACHE, _user_cache()):
+        try:
+            os.makedirs(d, exist_ok=True)
+            if os.access(d, os.W_OK):
+                return d
+        except OSError:
+            continue
+    return None
 
 
 def _version_tag() -> str:
@@ -166,34 +195,105 @@ def _headers_digest() -> str:
     return h.hexdigest()[:16]
 
 
-def code_object(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=None) -> Tuple[str, bytes]:
-    """(cache key, code object) of a plan, from the disk cache or compiled."""
-    src = plan_source(steps, in_cols, kind_set, levels)
-    key = hashlib.sha256("\n".join([src, " ".join(OPTIONS), _version_tag(), _headers_digest()]).encode()
-                         ).hexdigest()[:32]
-    d = _cache_dir()
-    path = os.path.join(d, f"{key}.hsaco") if d else None
-    if path and os.path.exists(path):
-        with open(path, "rb") as f:
-            STATS["disk_hits"] += 1
-            return key, f.read()
+def _source_key(src: str) -> str:
+    return hashlib.sha256("\n".join([src, " ".join(OPTIONS), _version_tag(), _headers_digest()]).encode()
+                          ).hexdigest()[:32]
+
+
+def _cached_code(key: str) -> Optional[bytes]:
+    code = _codes.get(key)
+    if code is not None:
+        return code
+    for d in _read_dirs():
+        p = os.path.join(d, f"{key}.hsaco")
+        if os.path.exists(p):
+            with open(p, "rb") as f:
+                STATS["disk_hits"] += 1
+                code = f.read()
+            _codes[key] = code
+            return code
+    return None
+
+
+def _compile_store(src: str, key: str) -> bytes:
+    """hiprtc compile + disk cache write (any thread: hiprtc runs without the GIL)."""
     t0 = time.perf_counter()
     code = compile_source(src)
-    STATS["compiled"] += 1
-    STATS["compile_s"] += time.perf_counter() - t0
-    if path:
-        tmp = f"{path}.{os.getpid()}.tmp"
+    dt = time.perf_counter() - t0
+    with _stats_lock:
+        STATS["compiled"] += 1
+        STATS["compile_s"] += dt
+    d = _cache_dir()
+    if d:
+        path = os.path.join(d, f"{key}.hsaco")
+        tmp = f"{path}.{os.getpid()}.{threading.get_ident()}.tmp"
         with open(tmp, "wb") as f:
             f.write(code)
         os.replace(tmp, path)
+    _codes[key] = code
+    return code
+
+
+def code_object(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=None) -> Tuple[str, bytes]:
+    """(cache key, code object) of a plan, from the memory / disk cache or compiled."""
+    src = plan_source(steps, in_cols, kind_set, levels)
+    key = _source_key(src)
+    code = _cached_code(key)
+    if code is None:
+        job = _jobs.get(key)
+        code = job.result() if job is not None else _compile_store(src, key)
     return key, code
 
 
+class _Job:
+    """One background hiprtc compile on a daemon thread (process exit does not wait for it)."""
+
+    def __init__(self, src: str, key: str):
+        self.done = threading.Event()
+        self.code: Optional[bytes] = None
+        self.error: Optional[BaseException] = None
+        threading.Thread(target=self._run, args=(src, key), daemon=True, name=f"vbn-hiprtc-{key[:8]}").start()
+
+    def _run(self, src, key):
+        try:
+            with _bg_slots:
+                self.code = _compile_store(src, key)
+        except BaseException as e:          # noqa: BLE001 -- reported to the launching thread
+            self.error = e
+        finally:
+            self.done.set()
+
+    def result(self) -> bytes:
+        self.done.wait()
+        if self.error is not None:
+            raise RuntimeError(f"background plan compile failed: {self.error}") from self.error
+        return self.code
+
+
+def pending() -> int:
+    """Background compiles not finished yet."""
+    return sum(1 for j in _jobs.values() if not j.done.is_set())
+
+
+def wait_pending(timeout: Optional[float] = None) -> bool:
+    """Wait for every background compile; True if none is left running."""
+    t_end = None if timeout is None else time.monotonic() + timeout
+    for j in list(_jobs.values()):
+        left = None if t_end is None else max(0.0, t_end - time.monotonic())
+        if not j.done.wait(left):
+            return False
+    return True
+
+
 def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_index: int,
-               plan_key: str, chain_waves: int = 0) -> Optional[int]:
-    """Loaded module handle for (plan, kind set, device), compiling on first use; None if the
-    plan cannot be specialised here (the caller runs the interpreter).  ``chain_waves`` > 0:
-    a Gibbs sweep table run on chain workgroups of that many waves (plan.gibbs_levels)."""
+               plan_key: str, chain_waves: int = 0, compile: str = "sync") -> Optional[int]:
+    """Loaded module handle for (plan, kind set, device); None if the plan cannot be specialised
+    here or is not ready (the caller runs the interpreter).  A code object in the memory or disk
+    cache is loaded right away; otherwise ``compile`` says what happens: "sync" compiles in this
+    call, "background" starts a hiprtc compile on a daemon thread (the module is used by the first
+    launch after it finishes; jit.wait_pending() joins), "never" only uses cached code.
+    ``chain_waves`` > 0: a Gibbs sweep table run on chain workgroups of that many waves
+    (plan.gibbs_levels)."""
     global _warned
     mk = (device_index, f"{plan_key}:{kind_set}:{chain_waves}")
     h = _modules.get(mk)
@@ -210,7 +310,21 @@ def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_ind
             if chain_waves > 0:
                 from .plan import gibbs_levels
                 levels = gibbs_levels(steps, in_cols, chain_waves)
-            _, code = code_object(steps, in_cols, kind_set, levels)
+            src = plan_source(steps, in_cols, kind_set, levels)
+            key = _source_key(src)
+            code = _cached_code(key)
+            if code is None:
+                job = _jobs.get(key)
+                if compile == "sync":
+                    code = job.result() if job is not None else _compile_store(src, key)
+                elif compile == "background" and job is None:
+                    _jobs[key] = _Job(src, key)
+                    STATS["background"] += 1
+                    return None
+                elif job is not None and job.done.is_set():
+                    code = job.result()
+                else:
+                    return None
             lib = _lib.load()
             handle = ctypes.c_void_p()
             buf = ctypes.create_string_buffer(code, len(code))

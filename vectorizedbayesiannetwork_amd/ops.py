@@ -45,24 +45,33 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
          fixed_ld: int, fixed_per_particle: bool, noise_b: int, n_noise: int, dmax: int,
          n_out_cols: int, mode: int, q_base: int, seed: int, offset: int,
          want_lp: bool, kind_mask: int = 63, wbuf: int = 0, plan_jit: int = 1,
-         precomp: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+         precomp: Optional[Tensor] = None, precomp_q: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
     """One particle walk over the whole step table (``wbuf``: floats per LDS weight buffer,
     >= every step's weight-block length).  ``plan_jit``: 0 = step-table interpreter, 1 = the
     plan-specialised walk (jit.py) for lean launches of >= jit.JIT_MIN_PARTICLES particles,
-    2 = for every lean launch.  ``precomp``: the per-sample quantities of the table's
-    VBN_F_PRECOMP steps ([S, stride], the pre-pass walk's out_x; plan.precompute_plans)."""
-    if precomp is not None:
+    2 = for every lean launch.  ``precomp`` / ``precomp_q``: the per-sample / per-query
+    quantities of the table's VBN_F_PRECOMP steps ([S, stride] / [B, stride_q], the pre-pass
+    walks' out_x; plan.precompute_plans)."""
+    for name, t, rows, attr in (("precomp", precomp, n_samples, "_vbn_precomp_stride"),
+                                ("precomp_q", precomp_q, n_queries, "_vbn_precomp_q_stride")):
+        need = getattr(steps, attr, None)
+        if t is None:
+            if need is not None:
+                raise ValueError(f"vbn_hip::walk: the step table reads {name} ({need} columns), none given")
+            continue
         if noise is not None:
             raise ValueError("vbn_hip::walk: precomputed quantities need a walk without injected draws")
-        if precomp.dim() != 2 or precomp.shape[0] != n_samples:
-            raise ValueError(f"vbn_hip::walk: precomp must be [{n_samples}, stride], got {tuple(precomp.shape)}")
-        need = getattr(steps, "_vbn_precomp_stride", None)
-        if need is not None and precomp.shape[1] != need:
-            raise ValueError(f"vbn_hip::walk: precomp has {precomp.shape[1]} columns, the step table reads {need}")
+        if n_samples % 64 != 0:
+            raise ValueError("vbn_hip::walk: precomputed quantities need a multiple of 64 samples per query")
+        if t.dim() != 2 or t.shape[0] != rows:
+            raise ValueError(f"vbn_hip::walk: {name} must be [{rows}, stride], got {tuple(t.shape)}")
+        if need is not None and t.shape[1] != need:
+            raise ValueError(f"vbn_hip::walk: {name} has {t.shape[1]} columns, the step table reads {need}")
+        _check_dev(name, t, torch.float32, params.device)
     return _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots,
                         max_out, fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode,
                         q_base, seed, offset, want_lp, kind_mask, precomp, 4 if precomp is not None else 0,
-                        0, -1, wbuf, plan_jit)
+                        0, -1, wbuf, plan_jit, precomp_q)
 
 
 @torch.library.custom_op("vbn_hip::walk_segment", mutates_args=("state",))
@@ -102,7 +111,8 @@ def _check_wbuf(op: str, steps: Tensor, begin: int, end: int, wbuf: int) -> None
 
 def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                  fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
-                 offset, want_lp, kind_mask, state, state_flags, step_begin, step_end, wbuf, plan_jit=0):
+                 offset, want_lp, kind_mask, state, state_flags, step_begin, step_end, wbuf, plan_jit=0,
+                 precomp_q=None):
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::walk runs on the GPU only (no CPU fallback); "
@@ -149,6 +159,7 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
     a.n_steps = step_end - step_begin
     a.state = _ptr(state) if state_flags else None
     a.state_flags = int(state_flags)
+    a.precomp_q = _ptr(precomp_q)
     a.n_slots = n_slots
     a.max_out = max_out
     a.fixed_ld = fixed_ld
@@ -180,13 +191,14 @@ LAST_WALK = {"specialised": False}
 
 def _plan_module(lib, a, steps, step_begin, step_end, work, plan_jit, device, chain_waves=0):
     """Module handle of the plan-specialised walk for this launch, or None (interpreter).
-    ``work`` = particles x sweeps; ``plan_jit`` 1 (auto: launches without injected draws of at
-    least jit.JIT_MIN_PARTICLES particle-steps) or 2 (always); ``chain_waves`` > 0: a Gibbs sweep
-    on chain workgroups of that many waves (:func:`gibbs_walk`)."""
+    ``work`` = particles x sweeps; ``plan_jit`` 1 (auto: launches without injected draws whose
+    plan is compiled; one of at least jit.JIT_MIN_PARTICLES particle-steps starts a missing
+    compile in the background) or 2 (always, compiling in the call); ``chain_waves`` > 0: a Gibbs
+    sweep on chain workgroups of that many waves (:func:`gibbs_walk`)."""
     if not plan_jit or step_begin != 0 or step_end != steps.shape[0]:
         return None
     from . import jit
-    if not jit.enabled() or (plan_jit == 1 and (a.noise or work < jit.JIT_MIN_PARTICLES)):
+    if not jit.enabled() or (plan_jit == 1 and a.noise):
         return None
     host = getattr(steps, "_vbn_host", None)
     if host is None:
@@ -194,14 +206,17 @@ def _plan_module(lib, a, steps, step_begin, step_end, work, plan_jit, device, ch
     km = lib.vbn_hip_walk_kind_set(ctypes.byref(a))
     if km <= 0:
         return None
+    # auto: a compiled plan serves every launch size (bit-identical outputs, so the choice never
+    # depends on how a batch is sharded); large launches start a missing compile in the background
+    compile = "sync" if plan_jit == 2 else ("background" if work >= jit.JIT_MIN_PARTICLES else "never")
     return jit.module_for(host[0], host[1], km, device.index if device.index is not None else 0, host[2],
-                          chain_waves)
+                          chain_waves, compile=compile)
 
 
 @walk.register_fake
 def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
-               offset, want_lp, kind_mask=63, wbuf=0, plan_jit=1, precomp=None):
+               offset, want_lp, kind_mask=63, wbuf=0, plan_jit=1, precomp=None, precomp_q=None):
     total = n_queries * n_samples
     lp = params.new_empty(total if want_lp else 0)
     x = params.new_empty((total, n_out_cols) if n_out_cols > 0 else (0,))
@@ -422,3 +437,208 @@ def posterior_stats(pdf: Tensor, samples: Tensor, eps: float) -> Tuple[Tensor, T
 def _posterior_stats_fake(pdf, samples, eps):
     b, d = pdf.shape[0], samples.shape[2]
     return pdf.new_empty(b, d), pdf.new_empty(b, d), pdf.new_empty(b)
+
+
+# ------------------------------------------------------------------------------------------
+# Query-level ops: a packed plan + evidence in, the engine's outputs out.
+#
+#   vbn_hip::pack_plan(steps[], in_cols[], out_cols[], meta) -> plan   (int32 host blob)
+#   vbn_hip::mcm(plan, params, fixed, n_samples, seed, ...)     -> (pdf [B,S], samples [B,S,Dt])
+#   vbn_hip::is_lw(plan, ..., lw_mode, normalize, eps)           -> (weights, samples, ess, fallback)
+#   vbn_hip::ancestral(plan, ...)                                -> samples [B,S,n_out]
+#
+# They replace the engine bodies of the reference (monte_carlo_marginalization.py:18-92,
+# importance_sampling.py:24-93 / likelihood_weighting.py:24-82, sampling/ancestral.py:13-65)
+# for an out-of-tree caller that holds a plan from VBN.pack_query: no Python engine, one call.
+# A plan blob holds up to four walk sections -- 0 the walk, 1 the same walk reading the
+# precomputed per-sample / per-query quantities, 2 the per-sample pre-pass, 3 the per-query
+# pre-pass (plan.precompute_plans) -- each [header 16 | steps n x 32 | in_cols | out_cols].
+# ------------------------------------------------------------------------------------------
+
+PLAN_MAGIC = 0x56424E50          # "VBNP"
+PLAN_SECTIONS = 4
+_SEC_META = 8                    # n_slots, max_out, fixed_ld, mode, kind_mask, wbuf, dmax, n_noise
+
+
+@torch.library.custom_op("vbn_hip::pack_plan", mutates_args=())
+def pack_plan(steps: list[Tensor], in_cols: list[Tensor], out_cols: list[Tensor], meta: list[int]) -> Tensor:
+    """Pack up to 4 walk sections into one int32 host tensor: [4 + 4 offsets] then per section
+    [magic, n_steps, n_in_cols, n_out_cols, 8 x meta, precomp stride, precomp_q stride, 0, 0 |
+    steps | in_cols | out_cols] (an empty steps tensor = absent section)."""
+    if not (len(steps) == len(in_cols) == len(out_cols)) or len(steps) > PLAN_SECTIONS:
+        raise ValueError("vbn_hip::pack_plan: steps / in_cols / out_cols lists of equal length <= 4")
+    if len(meta) != _SEC_META * len(steps):
+        raise ValueError(f"vbn_hip::pack_plan: meta needs {_SEC_META} ints per section")
+    from .plan import F_PRECOMP, F_PRECOMP_Q, S_AUX2, S_FLAGS
+    parts = [torch.tensor([PLAN_MAGIC, 1, len(steps), 0], dtype=torch.int32), torch.zeros(PLAN_SECTIONS, dtype=torch.int32)]
+    pos = 4 + PLAN_SECTIONS
+    offs = [0] * PLAN_SECTIONS
+    for i, (st, ic, oc) in enumerate(zip(steps, in_cols, out_cols)):
+        if st.numel() == 0:
+            continue
+        st = st.detach().to("cpu", torch.int32).reshape(-1, STEP_INTS)
+        ic = ic.detach().to("cpu", torch.int32).reshape(-1)
+        oc = oc.detach().to("cpu", torch.int32).reshape(-1)
+        fl, aux = st[:, S_FLAGS], st[:, S_AUX2]
+        pcs = ((fl & F_PRECOMP) != 0) & ((fl & F_PRECOMP_Q) == 0)
+        pcq = (fl & F_PRECOMP_Q) != 0
+        stride_s = int(aux[pcs][0]) >> 16 if bool(pcs.any()) else 0
+        stride_q = int(aux[pcq][0]) >> 16 if bool(pcq.any()) else 0
+        hdr = torch.tensor([PLAN_MAGIC, st.shape[0], ic.numel(), oc.numel(),
+                            *meta[_SEC_META * i:_SEC_META * (i + 1)], stride_s, stride_q, 0, 0], dtype=torch.int32)
+        offs[i] = pos
+        parts += [hdr, st.reshape(-1), ic, oc]
+        pos += hdr.numel() + st.numel() + ic.numel() + oc.numel()
+    parts[1] = torch.tensor(offs, dtype=torch.int32)
+    return torch.cat(parts)
+
+
+@pack_plan.register_fake
+def _pack_plan_fake(steps, in_cols, out_cols, meta):
+    n = 4 + PLAN_SECTIONS + sum(16 + s.numel() + i.numel() + o.numel()
+                                for s, i, o in zip(steps, in_cols, out_cols) if s.numel())
+    return torch.empty(n, dtype=torch.int32)
+
+
+_PLAN_DEV = {}          # (blob content hash, device) -> unpacked sections on the device
+
+
+def _unpack(plan: Tensor, device: torch.device):
+    """Plan blob -> per section (steps, in_cols, out_cols, header ints) on ``device`` (cached)."""
+    import hashlib
+    if plan.device.type != "cpu" or plan.dtype != torch.int32 or plan.dim() != 1:
+        raise ValueError("vbn_hip: plan must be the int32 host tensor of vbn_hip::pack_plan")
+    raw = plan.numpy()
+    key = (hashlib.sha1(raw.tobytes()).hexdigest(), str(device))
+    got = _PLAN_DEV.get(key)
+    if got is not None:
+        return got
+    if raw.size < 4 + PLAN_SECTIONS or int(raw[0]) != PLAN_MAGIC:
+        raise ValueError("vbn_hip: not a packed plan (bad magic)")
+    secs = []
+    for i in range(PLAN_SECTIONS):
+        o = int(raw[4 + i])
+        if o == 0:
+            secs.append(None)
+            continue
+        h = [int(x) for x in raw[o:o + 16]]
+        if h[0] != PLAN_MAGIC:
+            raise ValueError(f"vbn_hip: plan section {i} is corrupt")
+        n, nic, noc = h[1], h[2], h[3]
+        p = o + 16
+        st_np = raw[p:p + n * STEP_INTS].reshape(n, STEP_INTS).copy()
+        ic_np = raw[p + n * STEP_INTS:p + n * STEP_INTS + nic].copy()
+        oc_np = raw[p + n * STEP_INTS + nic:p + n * STEP_INTS + nic + noc].copy()
+        st = torch.from_numpy(st_np).to(device)
+        st._vbn_wblk_max = int(st_np[:, S_WBLK_LEN].max()) if n else 0
+        st._vbn_host = (st_np, ic_np, hashlib.sha1(st_np.tobytes() + b"|" + ic_np.tobytes()).hexdigest())
+        if h[12]:
+            st._vbn_precomp_stride = h[12]
+        if h[13]:
+            st._vbn_precomp_q_stride = h[13]
+        ic = torch.from_numpy(ic_np if nic else raw[:1].copy()).to(device)
+        oc = torch.from_numpy(oc_np if noc else raw[:1].copy()).to(device)
+        secs.append((st, ic, oc, h))
+    if len(_PLAN_DEV) > 256:
+        _PLAN_DEV.clear()
+    _PLAN_DEV[key] = secs
+    return secs
+
+
+def _section_walk(sec, params, fixed, b, n, seed, offset, q_base, noise, plan_jit, precomp=None, precomp_q=None):
+    st, ic, oc, h = sec
+    n_slots, max_out, fixed_ld, mode, kind_mask, wbuf, dmax, n_noise = h[4:12]
+    noise_b = int(noise.shape[2]) if noise is not None else 1
+    lp, x = walk(st, ic, params, fixed, noise, oc, b, n, n_slots, max_out, fixed_ld, False, noise_b,
+                 n_noise, dmax, h[3], mode, q_base, seed, offset, mode != 2, kind_mask, wbuf, plan_jit,
+                 precomp, precomp_q)
+    return lp, x
+
+
+def _query_walk(plan, params, fixed, n_samples, seed, offset, q_base, noise, plan_jit):
+    """The walk of a packed plan with its pre-passes (engines.run_walk's precompute rule)."""
+    device = params.device
+    secs = _unpack(plan, device)
+    if secs[0] is None:
+        raise ValueError("vbn_hip: plan has no walk section")
+    b = int(fixed.shape[0])
+    if fixed.dim() != 2 or fixed.shape[1] < secs[0][3][6]:
+        raise ValueError(f"vbn_hip: fixed must be [B, {secs[0][3][6]}] (plan fixed-buffer columns)")
+    fixed = fixed.to(device=device, dtype=torch.float32).contiguous()
+    if noise is not None:
+        noise = noise.to(device=device, dtype=torch.float32).contiguous()
+    use_pc = secs[1] is not None and noise is None and n_samples % 64 == 0
+    if not use_pc:
+        return _section_walk(secs[0], params, fixed, b, n_samples, seed, offset, q_base, noise, plan_jit), secs[0]
+    precomp = precomp_q = None
+    if secs[2] is not None:
+        _, x = _section_walk(secs[2], params, fixed, 1, n_samples, seed, offset, 0, None, 0)
+        precomp = x.view(n_samples, -1)
+    if secs[3] is not None:
+        _, x = _section_walk(secs[3], params, fixed, b, 64, seed, offset, q_base, None, 0)
+        precomp_q = x.view(b, 64, -1)[:, 0].contiguous()
+    return _section_walk(secs[1], params, fixed, b, n_samples, seed, offset, q_base, None, plan_jit,
+                         precomp, precomp_q), secs[1]
+
+
+@torch.library.custom_op("vbn_hip::mcm", mutates_args=())
+def mcm(plan: Tensor, params: Tensor, fixed: Tensor, n_samples: int, seed: int, offset: int = 0, q_base: int = 0,
+        noise: Optional[Tensor] = None, plan_jit: int = 1) -> Tuple[Tensor, Tensor]:
+    """Monte-Carlo marginalization of a packed MCM plan (VBN.pack_query): fixed [B, fixed_ld]
+    evidence / do values in the plan's column order -> (pdf [B,S], samples [B,S,Dt])."""
+    (lp, x), sec = _query_walk(plan, params, fixed, n_samples, seed, offset, q_base, noise, plan_jit)
+    if sec[3][7] != 0:
+        raise ValueError("vbn_hip::mcm: the plan is not an MCM walk")
+    b = int(fixed.shape[0])
+    return lp.view(b, n_samples), x.view(b, n_samples, -1)
+
+
+@mcm.register_fake
+def _mcm_fake(plan, params, fixed, n_samples, seed, offset=0, q_base=0, noise=None, plan_jit=1):
+    b = fixed.shape[0]
+    return params.new_empty(b, n_samples), params.new_empty(b, n_samples, 1)
+
+
+@torch.library.custom_op("vbn_hip::is_lw", mutates_args=())
+def is_lw(plan: Tensor, params: Tensor, fixed: Tensor, n_samples: int, seed: int, offset: int = 0,
+          q_base: int = 0, noise: Optional[Tensor] = None, lw_mode: bool = False, normalize: bool = True,
+          eps: float = 0.0, ess_threshold: float = 0.1, plan_jit: int = 1) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """Importance sampling (lw_mode False: the plan's roots drawn per query, evidence raw) or
+    likelihood weighting (True: shared roots, the caller clamps the evidence) of a packed
+    weighted plan -> (weights [B,S], samples [B,S,Dt], ess [B], fallback flag (device bool): IS
+    -- some ESS below max(1, ess_threshold S), NaN never triggers; LW -- False).  As the
+    reference, the fallback re-draw with LW is the caller's (its plan is another signature)."""
+    (lw, x), sec = _query_walk(plan, params, fixed, n_samples, seed, offset, q_base, noise, plan_jit)
+    if sec[3][7] != 1:
+        raise ValueError("vbn_hip::is_lw: the plan is not a weighted walk")
+    b = int(fixed.shape[0])
+    w, ess = normalize_weights(lw.view(b, n_samples), bool(normalize) or not lw_mode, float(eps))
+    if lw_mode:
+        flag = torch.zeros((), dtype=torch.bool, device=w.device)
+    else:
+        flag = (ess < max(1.0, float(ess_threshold) * n_samples)).any()
+    return w, x.view(b, n_samples, -1), ess, flag
+
+
+@is_lw.register_fake
+def _is_lw_fake(plan, params, fixed, n_samples, seed, offset=0, q_base=0, noise=None, lw_mode=False,
+                normalize=True, eps=0.0, ess_threshold=0.1, plan_jit=1):
+    b = fixed.shape[0]
+    return (params.new_empty(b, n_samples), params.new_empty(b, n_samples, 1), params.new_empty(b),
+            torch.empty((), dtype=torch.bool, device=params.device))
+
+
+@torch.library.custom_op("vbn_hip::ancestral", mutates_args=())
+def ancestral(plan: Tensor, params: Tensor, fixed: Tensor, n_samples: int, seed: int, offset: int = 0,
+              q_base: int = 0, noise: Optional[Tensor] = None, plan_jit: int = 1) -> Tensor:
+    """Ancestral sampling of a packed sample plan -> [B, S, n_out] (the plan's output nodes'
+    columns in topological order)."""
+    (_, x), sec = _query_walk(plan, params, fixed, n_samples, seed, offset, q_base, noise, plan_jit)
+    if sec[3][7] != 2:
+        raise ValueError("vbn_hip::ancestral: the plan is not a sampling walk")
+    return x.view(int(fixed.shape[0]), n_samples, -1)
+
+
+@ancestral.register_fake
+def _ancestral_fake(plan, params, fixed, n_samples, seed, offset=0, q_base=0, noise=None, plan_jit=1):
+    return params.new_empty(fixed.shape[0], n_samples, 1)

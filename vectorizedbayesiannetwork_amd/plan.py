@@ -45,14 +45,12 @@ KDE_CHUNKS = 16
 KDE_REC_TAIL = 8       # weight-0 record rows after the last point (csrc kde_scan prefetch)
 MLP_HIDDEN = (32, 32)
 # heads at least this wide run on the split-f16 MFMA (csrc head_mfma; cfg3 walk 2.97 -> 2.74 ms,
-# profiles/r03_bench/r03q_ab_cfg3.txt).  The hiprtc-compiled (plan-specialised) and
-# hipcc-compiled (interpreter) MFMA heads give IS / LW log-weights that differ by up to 3e-5
-# relative on evidence steps (profiles/r03n_headmfma_diag.txt); both are pinned to the oracle
-# per particle (tests/test_gpu_lean_parity.py).  1 << 30 turns the MFMA head off.
+# profiles/r03_bench/r03q_ab_cfg3.txt).  1 << 30 turns the MFMA head off.
 HEAD_MFMA_MIN = 8
 F_HEAD_MFMA = 4096
 F_PRECOMP = 8192          # csrc VBN_F_PRECOMP: per-sample quantities read from the pre-pass
 F_PRE_OUT = 16384         # csrc VBN_F_PRE_OUT: the pre-pass writes a node's per-sample quantities
+F_PRECOMP_Q = 32768       # csrc VBN_F_PRECOMP_Q: with F_PRECOMP, per-QUERY quantities (precomp_q)
 MAX_NODES = 1 << 14
 MAX_NODE_DIMS = 1 << 8
 
@@ -445,10 +443,12 @@ class QueryPlan:
     kind_mask: int = 63       # CPD kinds the walk evaluates (selects the kernel instantiation;
                               # | 32 non-relu activations, | 512 generic-MLP nodes)
     wbuf: int = 0             # floats per LDS weight buffer (max wblk_len over the steps)
-    # shared-sample precompute (precompute_plans): the same walk with VBN_F_PRECOMP steps, and
-    # the one-query pre-pass walk whose out_x they read
+    # precompute (precompute_plans): the same walk with VBN_F_PRECOMP steps, the one-query
+    # pre-pass walk whose out_x the per-sample ones read, and the one-wave-per-query pre-pass
+    # whose out_x the per-query (VBN_F_PRECOMP_Q) ones read
     pc: Optional["QueryPlan"] = None
     pre: Optional["QueryPlan"] = None
+    pre_q: Optional["QueryPlan"] = None
 
 
 def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
@@ -825,20 +825,31 @@ def precompute_width(packed: PackedModel, n: str) -> int:
 
 
 def precompute_plans(packed: PackedModel, plan: QueryPlan, *, skip: Sequence[str] = (),
-                     exact_f32: bool = False, kde_valu: bool = False) -> Optional[Tuple[QueryPlan, QueryPlan]]:
-    """Shared-sample precompute of a walk with shared root draws (MCM / LW / ancestral, Q5).
+                     exact_f32: bool = False, kde_valu: bool = False, per_query: bool = True
+                     ) -> Optional[Tuple[QueryPlan, Optional[QueryPlan], Optional[QueryPlan]]]:
+    """Per-sample and per-query precompute of a walk (SURVEY §7 hard part 5).
 
-    The root draws are shared by every query of the batch, so a node whose parents are all
-    latent roots sees the same inputs in every query of a sample: its MLP head outputs
-    (gaussian_nn, mdn, softmax_nn) or its KDE inverse-CDF chunk sums depend on the sample only.
-    A one-query pre-pass walk (the same root steps -- same flags, so the same Philox draws and
-    Box-Muller pairs -- then those nodes with VBN_F_PRE_OUT) computes them once per sample; the
-    main walk's steps for those nodes (VBN_F_PRECOMP) read them instead of recomputing them per
-    query, then run their epilogue and per-query draws as before.  Same device functions on
-    the same values: the outputs are bit-identical to the plain walk when every wave holds one
-    query (S a multiple of 64: the MLP's wave-uniform exact-path decision then sees the same
-    particles; run_walk checks).  Returns (main plan with VBN_F_PRECOMP, pre-pass plan), or
-    None when no node qualifies.
+    A node's MLP head outputs (gaussian_nn, mdn, softmax_nn; latent, or evidence with a
+    log-prob) or its KDE inverse-CDF chunk sums (latent kde) depend only on its parents'
+    values, which the reference broadcasts and recomputes for every particle
+    (``core/utils.py:64-69``, ``gaussian_nn.py:215-241``, ``kde.py:131-146``).  Two cases are
+    functions of fewer than B x S inputs:
+
+    * **per sample** -- parents all latent roots with draws shared by every query (MCM / LW /
+      ancestral, Q5): a one-query pre-pass walk (the same root steps -- same flags, so the same
+      Philox draws and Box-Muller pairs -- then those nodes with VBN_F_PRE_OUT) computes them
+      once per sample; the main walk's steps read row s (VBN_F_PRECOMP);
+    * **per query** -- parents all evidence / do values (every engine, IS included): a pre-pass
+      of one wave per query (B x 64 particles, every lane of a wave the same inputs) computes
+      them once per query; the main walk's steps read row b (VBN_F_PRECOMP | VBN_F_PRECOMP_Q,
+      wave-uniform scalar loads).
+
+    Either way the main walk then runs the node's epilogue and its own per-particle draws as
+    before.  Same device functions on the same values: the outputs are bit-identical to the
+    plain walk when every wave holds one query (S a multiple of 64: the MLP's wave-uniform
+    exact-path decision then sees the same inputs in the pre-pass wave and in the main wave;
+    run_walk checks).  Returns (main plan, per-sample pre-pass or None, per-query pre-pass or
+    None), or None when no node qualifies.
     """
     model = packed.model
     rows = plan.steps._vbn_host[0].copy()
@@ -847,45 +858,69 @@ def precompute_plans(packed: PackedModel, plan: QueryPlan, *, skip: Sequence[str
     at = {n: i for i, n in enumerate(order)}
     roots = [n for n in order if rows[at[n]][S_ROLE] == ROLE_LATENT and rows[at[n]][S_FLAGS] & F_SHARED]
     root_s = set(roots)
+    fixed = [n for n in order if rows[at[n]][S_ROLE] == ROLE_FIXED]
+    fixed_s = set(fixed)
     nn_kinds = (KIND_ID["gaussian_nn"], KIND_ID["mdn"], KIND_ID["softmax_nn"])
-    cand = []
-    for n in order:
+
+    def qualifies(n: str) -> bool:
         r = rows[at[n]]
         if r[S_FLAGS] & (F_ROOT | F_SHARED) or not model.parents[n]:
-            continue
-        if not all(p in root_s for p in model.parents[n]):
-            continue
+            return False
         kind, role = int(r[S_KIND]), int(r[S_ROLE])
-        if kind in nn_kinds and not r[S_FLAGS] & F_MLP_GENERIC and (
-                role == ROLE_LATENT or (role == ROLE_FIXED and r[S_FLAGS] & F_LOGP)):
-            cand.append(n)
-        elif (kind == KIND_ID["kde"] and role == ROLE_LATENT and not r[S_FLAGS] & F_KDE_VALU
-              and r[S_OFF_KQ] >= 0):
-            cand.append(n)
-    if not cand:
+        if kind in nn_kinds and not r[S_FLAGS] & F_MLP_GENERIC:
+            return role == ROLE_LATENT or (role == ROLE_FIXED and bool(r[S_FLAGS] & F_LOGP))
+        return (kind == KIND_ID["kde"] and role == ROLE_LATENT and not r[S_FLAGS] & F_KDE_VALU
+                and r[S_OFF_KQ] >= 0)
+
+    cand_s = [n for n in order if qualifies(n) and all(p in root_s for p in model.parents[n])]
+    cand_q = [n for n in order if per_query and qualifies(n) and all(p in fixed_s for p in model.parents[n])]
+    # an evidence candidate's pre-pass slot holds its head outputs, not its value: one that is a
+    # parent of another candidate stays per particle
+    cand_q = [n for n in cand_q if not (n in fixed_s and any(n in model.parents[m] for m in cand_q))]
+    if not cand_s and not cand_q:
         return None
-    keep = root_s | set(cand)
-    pre = build_plan(packed, latent=roots + cand, fixed=[], logp=[], out_nodes=cand, shared_roots=True,
-                     mode=MODE_SAMPLE, skip=[n for n in model.topo if n not in keep], exact_f32=exact_f32,
-                     pre_out=cand)
-    prow = pre.steps._vbn_host[0].copy()
-    porder = [n for n in model.topo if n in keep]
-    for i, n in enumerate(porder):                   # the main walk's Box-Muller pairs (roots pair
-        prow[i][S_FLAGS] &= ~(F_BM_FIRST | F_BM_SECOND)            # with roots only) and no others
-        if n in root_s:
-            prow[i][S_FLAGS] |= rows[at[n]][S_FLAGS] & (F_BM_FIRST | F_BM_SECOND)
-    pre = _with_steps(pre, prow, packed.device)
-    stride = int(pre.out_cols.numel())
-    col = 0
-    for n in cand:
-        r = rows[at[n]]
-        r[S_FLAGS] |= F_PRECOMP
-        r[S_AUX2] = col | (stride << 16)
-        col += precompute_width(packed, n)
-        r[S_WBLK_OFF] = 0                            # no MLP runs: nothing to stage
-        r[S_WBLK_LEN] = 0
-    assert col == stride and stride < (1 << 15)
-    return _with_steps(plan, rows, packed.device), pre
+    pre = pre_q = None
+    if cand_s:
+        keep = root_s | set(cand_s)
+        pre = build_plan(packed, latent=roots + cand_s, fixed=[], logp=[], out_nodes=cand_s, shared_roots=True,
+                         mode=MODE_SAMPLE, skip=[n for n in model.topo if n not in keep], exact_f32=exact_f32,
+                         pre_out=cand_s)
+        prow = pre.steps._vbn_host[0].copy()
+        porder = [n for n in model.topo if n in keep]
+        for i, n in enumerate(porder):               # the main walk's Box-Muller pairs (roots pair
+            prow[i][S_FLAGS] &= ~(F_BM_FIRST | F_BM_SECOND)        # with roots only) and no others
+            if n in root_s:
+                prow[i][S_FLAGS] |= rows[at[n]][S_FLAGS] & (F_BM_FIRST | F_BM_SECOND)
+        pre = _with_steps(pre, prow, packed.device)
+    if cand_q:
+        # the main walk's fixed nodes, reading the main walk's fixed buffer (its columns), then
+        # the candidates writing their quantities (an evidence candidate is one of them)
+        cq = set(cand_q)
+        keep = fixed_s | cq
+        pre_q = build_plan(packed, latent=cand_q, fixed=[n for n in fixed if n not in cq], logp=[],
+                           out_nodes=cand_q, shared_roots=False, mode=MODE_SAMPLE,
+                           skip=[n for n in model.topo if n not in keep], exact_f32=exact_f32, pre_out=cand_q)
+        qrow = pre_q.steps._vbn_host[0].copy()
+        qrow[:, S_FLAGS] &= ~(F_BM_FIRST | F_BM_SECOND)          # PRE_OUT steps draw no normals
+        qorder = [n for n in model.topo if n in keep]
+        for i, n in enumerate(qorder):
+            if n not in cq:
+                qrow[i][S_FIXEDCOL] = rows[at[n]][S_FIXEDCOL]
+        import dataclasses
+        pre_q = dataclasses.replace(_with_steps(pre_q, qrow, packed.device), fixed_nodes=list(plan.fixed_nodes),
+                                    fixed_ld=plan.fixed_ld)
+    for cands, extra in ((cand_s, 0), (cand_q, F_PRECOMP_Q)):
+        stride = sum(precompute_width(packed, n) for n in cands)
+        assert stride < (1 << 15)
+        col = 0
+        for n in cands:
+            r = rows[at[n]]
+            r[S_FLAGS] |= F_PRECOMP | extra
+            r[S_AUX2] = col | (stride << 16)
+            col += precompute_width(packed, n)
+            r[S_WBLK_OFF] = 0                        # no MLP runs: nothing to stage
+            r[S_WBLK_LEN] = 0
+    return _with_steps(plan, rows, packed.device), pre, pre_q
 
 
 def _with_steps(plan: QueryPlan, rows: np.ndarray, device) -> QueryPlan:
@@ -893,10 +928,12 @@ def _with_steps(plan: QueryPlan, rows: np.ndarray, device) -> QueryPlan:
     import dataclasses
     steps_t = torch.from_numpy(np.ascontiguousarray(rows)).to(device)
     steps_t._vbn_wblk_max = int(rows[:, S_WBLK_LEN].max()) if len(rows) else 0
-    pcm = (rows[:, S_FLAGS] & F_PRECOMP) != 0
-    if pcm.any():                                    # ops.walk checks the precomp tensor's width
-        steps_t._vbn_precomp_stride = int(rows[pcm, S_AUX2][0]) >> 16
+    pc = (rows[:, S_FLAGS] & F_PRECOMP) != 0
+    pq = (rows[:, S_FLAGS] & F_PRECOMP_Q) != 0
+    for m, attr in ((pc & ~pq, "_vbn_precomp_stride"), (pq, "_vbn_precomp_q_stride")):
+        if m.any():                                  # ops.walk checks the precomp tensors' widths
+            setattr(steps_t, attr, int(rows[m, S_AUX2][0]) >> 16)
     ic_host = plan.steps._vbn_host[1]
     steps_t._vbn_host = (rows.copy(), ic_host.copy(),
                          hashlib.sha1(rows.tobytes() + b"|" + ic_host.tobytes()).hexdigest())
-    return dataclasses.replace(plan, steps=steps_t, wbuf=steps_t._vbn_wblk_max, pc=None, pre=None)
+    return dataclasses.replace(plan, steps=steps_t, wbuf=steps_t._vbn_wblk_max, pc=None, pre=None, pre_q=None)
