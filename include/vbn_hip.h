@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 8
+#define VBN_ABI_VERSION 9
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001

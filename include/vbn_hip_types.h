@@ -67,6 +67,11 @@ enum vbn_role {
                                    the underflow shift (pass 1 is skipped)                    */
 #define VBN_F_PRE_OUT 16384     /* the pre-pass step of such a node: write those quantities to
                                    out_col .. (NN: n_out, kde: 17 slots) instead of a sample  */
+#define VBN_F_PRECOMP_Q 32768   /* with VBN_F_PRECOMP: the quantities are per QUERY -- the node's
+                                   parents are all evidence / do values -- computed once per
+                                   query by a pre-pass of one wave per query and read from
+                                   precomp_q [B][stride] (row b; aux2 as above); needs
+                                   n_samples a multiple of 64 (one query per wave)            */
 
 /* activations of the NN CPDs (reference gaussian_nn.py:19-24) */
 enum vbn_act { VBN_ACT_RELU = 0, VBN_ACT_TANH = 1, VBN_ACT_GELU = 2, VBN_ACT_ELU = 3 };
@@ -147,6 +152,8 @@ typedef struct vbn_walk_args {
                               launches too small to fill the chip (Gibbs at a few thousand
                               chains): lanes 32-63 mirror lanes 0-31 (same particle and draws,
                               no writes) and the MLPs run one 32-particle MFMA group   */
+  const float* precomp_q;  /* (ABI v9) per-query quantities of the VBN_F_PRECOMP_Q steps
+                              [B][stride] (read-only; lean walks, n_samples % 64 == 0), or NULL */
 } vbn_walk_args;
 
 #endif /* VBN_HIP_TYPES_H */

@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -68,6 +68,7 @@ class VbnWalkArgs(ctypes.Structure):
         ("n_noise", ctypes.c_int32),
         ("wbuf_floats", ctypes.c_int32),
         ("wave_particles", ctypes.c_int32),
+        ("precomp_q", ctypes.c_void_p),
     ]
 
 

@@ -323,6 +323,10 @@ static int walk_shape(const vbn_walk_args* a, walk_launch* out) {
   if ((a->state_flags & 4) && (!a->state || a->state_flags != 4 || a->noise || a->mode == VBN_MODE_GIBBS))
     return fail(VBN_E_ARGS, "vbn_hip_walk: state_flags 4 (precomputed per-sample quantities) needs a state "
                             "buffer and a walk without injected draws, segments or Gibbs sweeps");
+  if (a->precomp_q && (a->noise || a->mode == VBN_MODE_GIBBS || (a->n_samples % WAVE) != 0 ||
+                       a->wave_particles == 32 || (a->state && a->state_flags != 4)))
+    return fail(VBN_E_ARGS, "vbn_hip_walk: precomp_q (per-query quantities) needs a lean full-wave walk "
+                            "with n_samples a multiple of 64");
   if (a->wbuf_floats < 0 || (a->wbuf_floats % WBLK_CHUNK) != 0)
     return fail(VBN_E_ARGS, "vbn_hip_walk: wbuf_floats must be a non-negative multiple of 256");
   if (a->wave_particles != 0 && a->wave_particles != 32 && a->wave_particles != WAVE)

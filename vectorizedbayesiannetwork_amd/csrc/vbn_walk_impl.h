@@ -79,9 +79,17 @@ __device__ __forceinline__ float act_fn(float x) {
   return x > 0.f ? x : expm1f(x);  // ELU(alpha=1)
 }
 
+// Hardware transcendentals without the library's denormal / correctly-rounded fix-ups: the
+// natural log as v_log_f32 (log2) x ln 2 and the reciprocal as v_rcp_f32 (each ~1 ulp).  Only
+// for arguments that are normal floats by construction (the callers say why): __logf /
+// __fdividef / sqrtf lower to ~12-instruction sequences that handle denormal inputs, which
+// was ~10 % of the cfg2 walk's VALU stream (softplus and Box-Muller once per node).
+#define VBN_LN2_F 0.69314718055994530942f
+__device__ __forceinline__ float log_hw(float x) { return __builtin_amdgcn_logf(x) * VBN_LN2_F; }
+
 // F.softplus(beta=1, threshold=20) (reference cpds/utils.py:6-7) with hardware exp/log:
-// log1p(e) as Kahan's log(u) * e / (u - 1) (u - 1 is exact) for x >= -5, a 4-term series
-// below (relative error < 1e-9 there).
+// log1p(e) as Kahan's log(u) * e / (u - 1) (u - 1 is exact) for x >= -5 (u in [1, 2^29]:
+// normal), a 4-term series below (relative error < 1e-9 there).
 __device__ __forceinline__ float softplus_t(float x) {
 #ifdef VBN_ABL_NOSOFTPLUS
   return x;
@@ -90,7 +98,7 @@ __device__ __forceinline__ float softplus_t(float x) {
   const float e = __expf(x);
   if (x < -5.f) return e * (1.f - e * (0.5f - e * (0.33333334f - e * 0.25f)));
   const float u = 1.0f + e;
-  return __logf(u) * __fdividef(e, u - 1.0f);
+  return log_hw(u) * (e * __builtin_amdgcn_rcpf(u - 1.0f));   // u - 1 >= e^-5: normal
 }
 
 // Philox-2x32-10 counter-based RNG (Random123): counter (c0, c1), 32-bit key; one
@@ -107,11 +115,16 @@ __device__ __forceinline__ uint2 philox2x32(uint2 c, uint32_t k) {
 
 __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 
+// r = sqrt(-2 ln u1) with u1 in [2^-24, 1] (normal) on v_log_f32 / v_sqrt_f32 (-2 ln u1 in
+// [0, 33.3]: normal or 0)
+__device__ __forceinline__ float bm_radius(float u1) {
+  return __builtin_amdgcn_sqrtf(-2.0f * log_hw(u1));
+}
+
 __device__ __forceinline__ float box_muller(uint32_t a, uint32_t b) {
   const float u1 = (float)((a >> 8) + 1u) * (1.0f / 16777216.0f);  // (0,1]
   const float u2 = (float)(b >> 8) * (1.0f / 16777216.0f);
-  const float r = __builtin_sqrtf(-2.0f * __logf(u1));
-  return r * __builtin_amdgcn_cosf(u2);                              // cos(2*pi*u2)
+  return bm_radius(u1) * __builtin_amdgcn_cosf(u2);                 // cos(2*pi*u2)
 }
 
 struct Lane {
@@ -176,7 +189,7 @@ __device__ __forceinline__ float draw_normal(const vbn_walk_args& A, const vbn_s
   if (L.lean && d == 0 && (st.flags & VBN_F_BM_FIRST)) {
     const float u1 = (float)((w.x >> 8) + 1u) * (1.0f / 16777216.0f);
     const float u2 = (float)(w.y >> 8) * (1.0f / 16777216.0f);
-    const float r = __builtin_sqrtf(-2.0f * __logf(u1));
+    const float r = bm_radius(u1);
     L.bm_spare = r * __builtin_amdgcn_sinf(u2);
     return r * __builtin_amdgcn_cosf(u2);
   }
@@ -217,6 +230,16 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
 __device__ __forceinline__ const float* precomp_row(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
   const int col = st.aux2 & 0xffff, stride = (int)((unsigned)st.aux2 >> 16);
   return A.state + (int64_t)L.s * stride + col;
+}
+
+// VBN_F_PRECOMP | VBN_F_PRECOMP_Q: this query's row of the per-query pre-pass quantities
+// (precomp_q [B][stride]); one query per wave (host: n_samples % 64 == 0), so the row address is
+// wave-uniform and its reads are scalar loads
+__device__ __forceinline__ const cfloat* precomp_qrow(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
+  const int col = st.aux2 & 0xffff, stride = (int)((unsigned)st.aux2 >> 16);
+  const int64_t b = ((int64_t)__builtin_amdgcn_readfirstlane((int)(L.b >> 32)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane((int)L.b);
+  return CP(A.precomp_q) + b * stride + col;
 }
 
 // value of a fixed node: from the fixed buffer, or (VBN_F_KEEP, Gibbs) the slot's current value
@@ -728,10 +751,15 @@ __device__ __forceinline__ void run_mlp_generic(const vbn_walk_args& A, const vb
 template <unsigned KM, int NOUT = 0, typename F>
 __device__ __forceinline__ void run_mlp(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
   constexpr bool MIR = (KM & 64) != 0;             // half-wave instantiation
-  if (st.flags & VBN_F_PRECOMP) {                  // parents = shared root draws: this sample's
-    const float* __restrict__ q = precomp_row(A, st, L);   // head outputs from the pre-pass
-    pre();
-    for (int j = 0; j < st.n_out; ++j) L.scr[j * WAVE + L.lane] = q[j];
+  if (st.flags & VBN_F_PRECOMP) {                  // parents = shared root draws / evidence: this
+    pre();                                         // sample's / query's head outputs, pre-pass
+    if (st.flags & VBN_F_PRECOMP_Q) {
+      const cfloat* q = precomp_qrow(A, st, L);
+      for (int j = 0; j < st.n_out; ++j) L.scr[j * WAVE + L.lane] = q[j];
+    } else {
+      const float* __restrict__ q = precomp_row(A, st, L);
+      for (int j = 0; j < st.n_out; ++j) L.scr[j * WAVE + L.lane] = q[j];
+    }
     wave_sync();
     return;
   }
@@ -825,7 +853,7 @@ __device__ __forceinline__ void step_gaussian_nn(const vbn_walk_args& A, const v
     vwrite(L, st.out_col + d, x);
     if (want_lp) {
       const float diff = x - loc;
-      acc += (diff * diff) / (scale * scale) + 2.0f * __logf(scale) + LOG_2PI_F;
+      acc += (diff * diff) / (scale * scale) + 2.0f * log_hw(scale) + LOG_2PI_F;   // scale >= min_scale std_y
     }
   }
   if (want_lp) lp += -0.5f * acc;
@@ -1396,14 +1424,24 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   const float negsq = kde_own(L, slots, scl, nf, xv);
   const bool pre = (st.flags & VBN_F_PRECOMP) != 0;
   float shift = 0.f;
-  if (pre) {                                          // pass 1 of this sample from the pre-pass
-    const float* __restrict__ q = precomp_row(A, st, L);
-    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-      const float cs = q[ch];
-      L.scr[ch * WAVE + lane] = cs;
-      tot += (double)cs;
+  if (pre) {                                          // pass 1 of this sample / query, pre-pass
+    if (st.flags & VBN_F_PRECOMP_Q) {
+      const cfloat* q = precomp_qrow(A, st, L);
+      for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+        const float cs = q[ch];
+        L.scr[ch * WAVE + lane] = cs;
+        tot += (double)cs;
+      }
+      shift = q[KDE_CHUNKS];
+    } else {
+      const float* __restrict__ q = precomp_row(A, st, L);
+      for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+        const float cs = q[ch];
+        L.scr[ch * WAVE + lane] = cs;
+        tot += (double)cs;
+      }
+      shift = q[KDE_CHUNKS];
     }
-    shift = q[KDE_CHUNKS];
   } else
 #ifdef VBN_ABL_NOP1
   if (true) {
