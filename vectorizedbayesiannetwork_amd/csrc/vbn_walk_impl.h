@@ -654,13 +654,20 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
   }
 }
 
+// Non-relu activations (kind-set bit 5) take the generic fan-in loop only: a compile-time fan-in
+// per activation multiplied the inlined MLP copies of those kind sets by 4 (their objects took
+// ~40 min each to build); relu -- the reference default and every benchmark DAG -- keeps them.
 template <int ACT, bool STD, bool MIR, int NOUT, typename F>
 __device__ __forceinline__ void mlp_nin(const vbn_walk_args& A, const vbn_step& st, const Lane& L, F&& pre) {
+  if constexpr (ACT != VBN_ACT_RELU) {
+    mlp_forward<ACT, STD, 0, MIR, NOUT>(A, st, L, pre);
+  } else {
   switch (st.n_in) {
     case 1: mlp_forward<ACT, STD, 1, MIR, NOUT>(A, st, L, pre); break;
     case 2: mlp_forward<ACT, STD, 2, MIR, NOUT>(A, st, L, pre); break;
     case 3: mlp_forward<ACT, STD, 3, MIR, NOUT>(A, st, L, pre); break;
     default: mlp_forward<ACT, STD, 0, MIR, NOUT>(A, st, L, pre); break;
+  }
   }
 }
 
@@ -950,7 +957,7 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
     lsum = 0.f;
     for (int k = 0; k < K; ++k) lsum += __expf(scr[k * WAVE + lane] - lmax);
     psum = 0.f;
-    const float rl = 1.0f / lsum;
+    const float rl = __builtin_amdgcn_rcpf(lsum);     // lsum >= 1
     for (int k = 0; k < K; ++k) {
       const float p = fmaxf(__expf(scr[k * WAVE + lane] - lmax) * rl, 1e-5f);
       scr[k * WAVE + lane] = p;
@@ -1017,13 +1024,13 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
           ls = t[2 * K + 2 * K * D + k * D + d];
           var = t[2 * K + 3 * K * D + k * D + d];
         } else {
-          ls = __logf(scale_kd(k, d));
+          ls = log_hw(scale_kd(k, d));                 // scale >= min_scale
           var = __expf(2.0f * ls);
         }
         const float diff = x - loc_kd(k, d);
         acc += (diff * diff) / var + 2.0f * ls + LOG_2PI_F;
       }
-      const float lpi = root ? t[K + k] : __logf(pi_k(k));
+      const float lpi = root ? t[K + k] : log_hw(pi_k(k));   // pi >= 1e-5 / sum
       const float term = lpi + (-0.5f * acc);
       if (term == -INFINITY) continue;
       if (term > m) {
@@ -1033,7 +1040,7 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
         se += __expf(term - m);
       }
     }
-    lp += (m == -INFINITY) ? m : m + __logf(se);
+    lp += (m == -INFINITY) ? m : m + log_hw(se);          // se >= 1
   }
 }
 
@@ -1086,11 +1093,11 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
         // the logits are not read again: the class probabilities replace them, computed once
         // (the inverse CDF reads each twice; same operations, so the same values); one
         // reciprocal of the sum instead of C divisions
-        const float rse = 1.0f / se;
+        const float rse = __builtin_amdgcn_rcpf(se);  // se >= 1
         for (int c = 0; c < C; ++c) L.scr[(d * C + c) * WAVE + lane] = __expf(logit(c) - m) * rse;
         idx = inv_cdf(C, uu.x, [&](int c) { return L.scr[(d * C + c) * WAVE + lane]; });
       } else {
-        const float rse = 1.0f / se;
+        const float rse = __builtin_amdgcn_rcpf(se);  // se >= 1
         idx = inv_cdf(C, uu.x, [&](int c) { return __expf(logit(c) - m) * rse; });
       }
       const float left = e[idx];
@@ -1129,7 +1136,7 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
         for (int c = 0; c <= C; ++c) cnt += (x >= e[c]) ? 1 : 0;
         bin = min(max(cnt - 1, 0), C - 1);
       }
-      const float log_bin = logit(bin) - m - __logf(se);
+      const float log_bin = logit(bin) - m - log_hw(se);
       float lw = 0.f;
       if (!disc) {
         const float left = e[bin];
@@ -1139,19 +1146,19 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
         const float xu = clip ? fminf(fmaxf(x, left), right) : x;
         const bool inside = (x >= left) && (x <= right);
         if (mode == VBN_WITHIN_UNIFORM) {
-          lw = -logf(width);
+          lw = -log_hw(width);
           if (!clip && !inside) lw = -INFINITY;
         } else if (mode == VBN_WITHIN_TRIANGULAR) {
           const float dl = fmaxf(width * (center - left), min_bw2);
           const float dr = fmaxf(width * (right - center), min_bw2);
           float pdf = (xu <= center) ? 2.0f * (xu - left) / dl : 2.0f * (right - xu) / dr;
           pdf = fmaxf(pdf, 0.0f);
-          lw = logf(fmaxf(pdf, 1e-12f));
+          lw = log_hw(fmaxf(pdf, 1e-12f));
           if (!clip && !inside) lw = -INFINITY;
         } else {
           const float sigma = fmaxf(wscale * width, min_bw);
           const float diff = xu - center;
-          lw = -(diff * diff) / (2.0f * (sigma * sigma)) - logf(sigma) - 0.91893853320467274178f;
+          lw = -(diff * diff) / (2.0f * (sigma * sigma)) - log_hw(sigma) - 0.91893853320467274178f;
         }
       }
       lp_acc += log_bin + lw;
