@@ -330,12 +330,16 @@ def main():
     assert bool(ops.LAST_WALK.get("specialised")) == specialised, "kernel timing ran another walk form"
     kernel_name = "vbn_walk_plan" if specialised else "vbn_walk_kernel"
     precomputed = bool(E.LAST_LAUNCH.get("precomputed"))
-    n_precomp = 0
+    n_pre_s = n_pre_q = 0
     if precomputed:
-        # nodes with shared-root parents computed once per sample: the HIP-event interval holds
-        # the one-query pre-pass launch as well as the walk (plan.precompute_plans)
-        kernel_name += " + shared-sample pre-pass (vbn_walk_kernel, 1 query)"
-        n_precomp = int(((plan.pc.steps[:, 2] & 8192) != 0).sum().item())
+        # nodes with shared-root parents computed once per sample, nodes with evidence parents
+        # once per query: the HIP-event interval holds both pre-pass launches as well as the
+        # walk (plan.precompute_plans)
+        fl = plan.pc.steps[:, 2]
+        n_pre_q = int(((fl & 32768) != 0).sum().item())
+        n_pre_s = int(((fl & 8192) != 0).sum().item()) - n_pre_q
+        kernel_name += (" + pre-passes (vbn_walk_kernel: " + ", ".join(
+            t for t, n in (("per-sample, 1 query", n_pre_s), ("per-query, B x 64", n_pre_q)) if n) + ")")
 
     # the host path's own settling (caching allocator, Python-side caches) before the W warmup
     # steps: ~50 ms of untimed infer_posterior calls, like the walks of the kernel timing above
@@ -470,7 +474,7 @@ def main():
                             else "step-table interpreter"),
                    "plan_compile_s": round(jit.STATS["compile_s"], 2), "plan_cache_hits": jit.STATS["disk_hits"],
                    "first_call_s": round(t_first, 2), "background_compile_wait_s": round(t_wait, 2),
-                   "shared_sample_precompute_nodes": n_precomp},
+                   "precompute_nodes": {"per_sample": n_pre_s, "per_query": n_pre_q}},
         "roofline": roof,
     }
     if fallbacks:

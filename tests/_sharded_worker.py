@@ -17,6 +17,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 B, S = 64, 1024
+B_BIG = 1536                 # cfg3 IS: 1.5 M particles in one process (>= jit.JIT_MIN_PARTICLES), 0.75 M per rank
 HOT_NODE_VALUE = 50.0        # off-manifold evidence in the last query (rank 1's shard): ESS ~ 1
 
 
@@ -71,6 +72,16 @@ def main():
         torch.cuda.synchronize()
         res["ancestral"] = {"seeds": [sh.last_seed], "fallback": False, "pdf": None,
                             "xs": None if xs is None else xs.cpu()}
+        # a batch whose single-process launch runs the plan-specialised walk while each rank's
+        # half runs the step-table interpreter (forced): the gathered result must not depend on it
+        from vectorizedbayesiannetwork_amd.engines import ImportanceSampling
+        model3, vbn3, target3, ev3 = synthetic_workload("cfg3", B_BIG, "cuda")
+        torch.manual_seed(1000 + a.rank)
+        sh = ShardedEngine(ImportanceSampling(n_samples=S, plan_jit=False), gather=True)
+        pdf, xs = sh.infer_posterior(vbn3, Query(target3, {k: v.cuda() for k, v in ev3.items()}))
+        torch.cuda.synchronize()
+        res["is_big_cfg3"] = {"seeds": [sh.last_seed], "fallback": bool(sh.engine._last_fallback),
+                              "pdf": None if pdf is None else pdf.cpu(), "xs": None if xs is None else xs.cpu()}
         torch.save(res, a.out)
         dist.barrier()
     finally:

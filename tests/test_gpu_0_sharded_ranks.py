@@ -65,6 +65,37 @@ def _reference(name, seed):
     raise KeyError(name)
 
 
+def _reference_big(seed):
+    """cfg3 IS over the whole 1536-query batch in one process, auto mode: >= 2^20 particles, so
+    the plan-specialised walk (compiled before the timed call if it was not cached)."""
+    sys.path.insert(0, HERE)
+    import _sharded_worker as W
+    from workloads import synthetic_workload
+    from vectorizedbayesiannetwork_amd import jit, ops
+    from vectorizedbayesiannetwork_amd.engines import ImportanceSampling, Query
+    model, vbn, target, ev = synthetic_workload("cfg3", W.B_BIG, "cuda")
+    q = Query(target, {k: v.cuda() for k, v in ev.items()})
+    ImportanceSampling(n_samples=W.S).infer_posterior(vbn, q, seed=seed)
+    jit.wait_pending()
+    eng = ImportanceSampling(n_samples=W.S)
+    pdf, xs = eng.infer_posterior(vbn, q, seed=seed)
+    torch.cuda.synchronize()
+    return pdf.cpu(), xs.cpu(), bool(eng._last_fallback), bool(ops.LAST_WALK.get("specialised"))
+
+
+def test_sharded_interpreter_equals_single_process_specialised(rank_results):
+    """The plan-specialised / interpreter choice never changes results: rank halves
+    on the interpreter gather to exactly the single-process specialised walk (split-f16 MFMA
+    heads included: cfg3 is mdn + softmax_nn)."""
+    from vectorizedbayesiannetwork_amd import jit
+    r0, r1 = rank_results[0]["is_big_cfg3"], rank_results[1]["is_big_cfg3"]
+    assert r0["seeds"] == r1["seeds"] and r1["xs"] is None
+    pdf, xs, fb, spec = _reference_big(r0["seeds"][-1])
+    assert spec or not jit.enabled(), "the single-process reference did not run the specialised walk"
+    assert r0["fallback"] == fb
+    assert torch.equal(r0["xs"], xs) and torch.equal(r0["pdf"], pdf)
+
+
 @pytest.mark.parametrize("name", ["mcm", "mcm_overlap", "is", "is_hot", "ancestral"])
 def test_two_ranks_match_single_process(rank_results, name):
     r0, r1 = rank_results[0][name], rank_results[1][name]
