@@ -482,10 +482,16 @@ def main():
     if gather_info is not None:
         out["gather"] = gather_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # a bounded sample of ~10-30 s of CPU work (the oracle's q/s is linear in B): cfg2 /
+        # anchor64 1024 queries, cfg3 (IS, ~100 q/s) 256, cfg5 (~0.7 q/s) 8, cfg4 (~0.2 q/s) 2
         kde = "kde" in cfg["kinds"]
-        nq = args.cpu_queries or (1024 if cfg["engine"] == "monte_carlo_marginalization" and cfg["n_nodes"] <= 64
-                                  and not kde else (1 if kde else 8))
-        reps_cpu = 1 if kde else args.cpu_reps
+        if args.cpu_queries:
+            nq = args.cpu_queries
+        elif kde:
+            nq = 2 if cfg["kinds"] == ("kde",) else 8
+        else:
+            nq = 1024 if cfg["engine"] == "monte_carlo_marginalization" else 256
+        reps_cpu = 2 if kde else args.cpu_reps
         print(f"cpu baseline: {nq} queries in a child process ...", file=sys.stderr, flush=True)
         out["cpu_baseline"] = cpu_baseline(args.config, nq, reps_cpu)
     if rank == 0:
