@@ -220,6 +220,13 @@ def load_traffic(cfg_name: str):
 
 
 KT_UNTIMED, KT_TIMED = 64, 20     # roofline kernel timing: untimed launches, then timed ones
+_T0 = time.perf_counter()
+
+
+def log(msg: str) -> None:
+    """progress on stderr (the JSON line is the only stdout output)"""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s rank {os.environ.get('RANK', '0')}] {msg}",
+          file=sys.stderr, flush=True)
 
 
 def main():
@@ -269,6 +276,7 @@ def main():
         torch.cuda.set_device(0)
     device = f"cuda:{local}"
 
+    log(f"world {world}, backend {args.dist_backend if dist else '-'}, device {device}: building {args.config}")
     cfg, model, vbn, query = build_workload(args.config, device, world)
     B, S = cfg["B"], cfg["S"]                         # B = queries per GPU
     extra = {"n_particles": S} if cfg["engine"] == "rao_blackwellized_marginalization" else {}
@@ -292,6 +300,7 @@ def main():
     # the timed region (the first ~25 walks after idle run up to 17 % slower)
     from vectorizedbayesiannetwork_amd import engines as E
     from vectorizedbayesiannetwork_amd import jit, ops
+    log("first call")
     t_first = time.perf_counter()
     vbn.infer_posterior(query)                # builds the plan of the timed steps
     sharded.wait()
@@ -310,6 +319,7 @@ def main():
     pk, plan, fixed = last["pk"], last["plan"], last["fixed"]
     stream = torch.cuda.current_stream()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    log("kernel timing")
     ev0.record(stream)
     E.run_walk(pk, plan, fixed, B, S, seed=1000)
     ev1.record(stream)
@@ -345,6 +355,7 @@ def main():
     # steps: ~50 ms of untimed infer_posterior calls, like the walks of the kernel timing above
     # (a 20-step window right after a handful of calls measured 0.92 vs 0.82 ms per step in
     # steady state, profiles/r03_bench/r03t_blocks.txt)
+    log(f"kernel {kern_ms:.4f} ms; settling calls")
     for _ in range(max(5, min(200, math.ceil(50.0 / kern_ms)))):
         vbn.infer_posterior(query)
     sharded.wait()
@@ -361,6 +372,7 @@ def main():
     # in a short timed loop, while the host is only a step or two ahead, idles the GPU.  No
     # gc.collect() here: a full collection right before t0 idles the GPU for long enough that
     # its clocks drop (0.976 vs 0.813 ms per step over the driver's 20 steps)
+    log("timed region")
     gc.disable()
     barrier()
     torch.cuda.synchronize()
@@ -401,6 +413,7 @@ def main():
                               device=device if args.dist_backend == "nccl" else "cpu")
             tdist.all_reduce(dt, op=tdist.ReduceOp.MAX)
             return 1e3 * float(dt.item()) / n
+        log("gather accounting")
         n_g = max(5, min(args.steps, 20))
         b0 = sharded.gather_bytes
         walk_only = window(n_g, False, False)

@@ -30,6 +30,7 @@ def main():
     from vectorizedbayesiannetwork_amd import engines as E
 
     torch.cuda.set_device(0)
+    E.PRECOMPUTE = False             # the variants are compiled from the plain plan (jit_variants.py)
     cfg, model, vbn, query = build_workload(a.config, "cuda:0", 1)
     B, S = cfg["B"], cfg["S"]
     vbn.set_inference_method(cfg["engine"], n_samples=S, plan_jit=False)
@@ -63,7 +64,7 @@ def main():
     captured = {}
     orig = J.module_for
 
-    def capture(steps, in_cols, kind_set, dev, key, *rest):
+    def capture(steps, in_cols, kind_set, dev, key, *rest, **kw):
         captured["km"] = kind_set
         return None
     J.module_for = capture

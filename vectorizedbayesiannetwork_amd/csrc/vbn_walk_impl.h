@@ -102,12 +102,12 @@ __device__ __forceinline__ float softplus_t(float x) {
 }
 
 // Philox-2x32-10 counter-based RNG (Random123): counter (c0, c1), 32-bit key; one
-// v_mad_u64_u32 per round.
+// v_mad_u64_u32 and one three-input XOR (gfx950 v_bitop3_b32, truth table 0x96) per round.
 __device__ __forceinline__ uint2 philox2x32(uint2 c, uint32_t k) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p = (uint64_t)0xD256D193u * c.x;
-    c = make_uint2((uint32_t)(p >> 32) ^ k ^ c.y, (uint32_t)p);
+    c = make_uint2(__builtin_amdgcn_bitop3_b32((uint32_t)(p >> 32), k, c.y, 0x96), (uint32_t)p);
     k += 0x9E3779B9u;
   }
   return c;
@@ -908,6 +908,9 @@ __device__ __forceinline__ void step_linear_gaussian(const vbn_walk_args& A, con
 // ------------------------------------------------------------------------------------------
 // categorical inverse-CDF: smallest k with cumsum(p)[k] > u * sum(p)
 // ------------------------------------------------------------------------------------------
+// Without an early exit: the first crossing is kept by selects, so a wave whose lanes cross at
+// different k runs one straight pass instead of a divergent loop (the divergent form held the
+// mdn / softmax_nn epilogues' values live across exec-mask joins: cfg3 spilled 46 VGPRs)
 template <typename F>
 __device__ __forceinline__ int inv_cdf(int K, float u, F prob) {
   float tot = 0.f;
@@ -915,9 +918,12 @@ __device__ __forceinline__ int inv_cdf(int K, float u, F prob) {
   const float thr = u * tot;
   float cum = 0.f;
   int idx = K - 1;
+  bool found = false;
   for (int k = 0; k < K - 1; ++k) {
     cum += prob(k);
-    if (cum > thr) { idx = k; break; }
+    const bool hit = !found && cum > thr;
+    idx = hit ? k : idx;
+    found |= hit;
   }
   return idx;
 }
@@ -1296,11 +1302,25 @@ __device__ __forceinline__ float kde_reduce_tiles(const float (&s)[4], int lane)
   return k + __shfl_xor(o, 16);
 }
 
+// Point operands are prefetched a whole trip ahead, across chunk boundaries: the packs of a
+// 64-node M = 10,000 DAG (~5 MB) do not stay in one XCD's 4 MiB L2 while ~4,000 resident waves
+// walk different nodes, so most operand loads are served by the Infinity Cache (cfg4: 78 GB
+// of L2 fills per launch, r04 PMC), ~545+ cycles away -- more than one block of work covers.
+
+// first four 16-point blocks of a pass over pack kq starting at block b0 (blast = last block)
+__device__ __forceinline__ void kde_prefetch4(const float* __restrict__ kq, int b0, int blast, int lane,
+                                              float (&nx)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) nx[u] = kq[min(b0 + u, blast) * 64 + lane];
+}
+
 // per-lane partial sums of exp2(arg) over 16-point blocks [b0, b1) of pack kq, b1 - b0 a
-// multiple of 4 (padding blocks have weight 0); sums in packed pairs (v_pk_add_f32)
+// multiple of 4 (padding blocks have weight 0); sums in packed pairs (v_pk_add_f32).  nx holds
+// blocks b0 .. b0+3 on entry (kde_prefetch4) and b1 .. b1+3 on return: each trip loads the
+// next trip's four operands before its 16 MFMAs and 64 exps.
 template <bool ZC>
-__device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int b0, int b1, const KdeOps& o,
-                                              int lane, float (&s)[4]) {
+__device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int b0, int b1, int blast,
+                                              const KdeOps& o, int lane, float (&s)[4], float (&nx)[4]) {
   f32x4 cin[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -1309,9 +1329,9 @@ __device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int 
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x2{0.f, 0.f};
   for (int b = b0; b < b1; b += 4) {
-    float a[4];
+    const float a[4] = {nx[0], nx[1], nx[2], nx[3]};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) a[u] = kq[(b + u) * 64 + lane];   // four loads in flight
+    for (int u = 0; u < 4; ++u) nx[u] = kq[min(b + 4 + u, blast) * 64 + lane];   // next trip's operands
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       f32x4 d[4];
@@ -1329,10 +1349,10 @@ __device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int 
   for (int t = 0; t < 4; ++t) s[t] += acc[t].x + acc[t].y;
 }
 
-__device__ __forceinline__ void kde_sums(const float* __restrict__ kq, int b0, int b1, const KdeOps& o, int nf,
-                                         int lane, float (&s)[4]) {
-  if (nf <= 2) kde_mfma_sums<true>(kq, b0, b1, o, lane, s);
-  else kde_mfma_sums<false>(kq, b0, b1, o, lane, s);
+__device__ __forceinline__ void kde_sums(const float* __restrict__ kq, int b0, int b1, int blast, const KdeOps& o,
+                                         int nf, int lane, float (&s)[4], float (&nx)[4]) {
+  if (nf <= 2) kde_mfma_sums<true>(kq, b0, b1, blast, o, lane, s, nx);
+  else kde_mfma_sums<false>(kq, b0, b1, blast, o, lane, s, nx);
 }
 
 // One-feature nodes: pass-1 sums on v_mfma_f32_32x32x2_f32 (1024 pairs per instruction, half
@@ -1340,39 +1360,46 @@ __device__ __forceinline__ void kde_sums(const float* __restrict__ kq, int b0, i
 // [block32][2][32]), columns = the 32 particles of tile t (B = (2x', -1)), C = -|x'|^2, i.e.
 // d = fmaf(|y'|^2, -1, fmaf(y', 2x', -|x'|^2)) (kde_arg_rec with nf < 0 replicates it).  Lane
 // (h, n) sums the exps of rows row(r, h) for particle 32 t + n; the two halves of both tiles
-// are added with one v_permlane32_swap per chunk.
-__device__ __forceinline__ void kde_mfma32_sums(const float* __restrict__ kq32, int b0, int b1, float bt0, float bt1,
-                                                float ct0, float ct1, int lane, float (&s)[2]) {
+// are added with one v_permlane32_swap per chunk.  pa = kq32 + lane; r = a ring of the next
+// three 32-point blocks' operands (blocks b0 .. b0+2 on entry, b1 .. b1+2 on return), so each
+// load is issued three blocks (~6 MFMAs and 48 exps of this wave) before its use.
+__device__ __forceinline__ void kde_mfma32_sums(const float* __restrict__ pa, int b0, int b1, int blast,
+                                                float bt0, float bt1, float ct0, float ct1, float (&s)[2],
+                                                float (&r)[3]) {
   f32x16 c0, c1;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { c0[r] = ct0; c1[r] = ct1; }
+  for (int i = 0; i < 16; ++i) { c0[i] = ct0; c1[i] = ct1; }
   f32x2 acc0 = f32x2{0.f, 0.f}, acc1 = f32x2{0.f, 0.f};
-  // software pipeline: the exps of one MFMA run while the next MFMA is in the matrix pipe,
-  // the point operand two blocks ahead is in flight
   if (b1 <= b0) return;
-  const float* __restrict__ pa = kq32 + b0 * 64 + lane;
-  const int nb = b1 - b0;
-  float an = pa[nb > 1 ? 64 : 0];
-  f32x16 q = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[0], bt1, c1, 0, 0, 0);
-  f32x16 d = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[0], bt0, c0, 0, 0, 0);
+  auto take = [&](int i) {                     // block i's operand; block i + 3's load issued
+    const float a = r[0];
+    r[0] = r[1];
+    r[1] = r[2];
+    r[2] = pa[min(i + 3, blast) * 64];
+    return a;
+  };
+  // software pipeline: the exps of one MFMA run while the next MFMA is in the matrix pipe
+  const float a0 = take(b0);
+  f32x16 q = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bt1, c1, 0, 0, 0);
+  f32x16 d = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bt0, c0, 0, 0, 0);
 #pragma unroll
-  for (int r = 0; r < 16; r += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[r]), __builtin_amdgcn_exp2f(d[r + 1])};
-  for (int i = 1; i < nb; ++i) {
-    const float a = an;
-    an = pa[min(i + 1, nb - 1) * 64];
+  for (int i = 0; i < 16; i += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[i]), __builtin_amdgcn_exp2f(d[i + 1])};
+#pragma unroll 3
+  for (int i = b0 + 1; i < b1; ++i) {
+    const float a = take(i);
     __builtin_amdgcn_sched_barrier(0);
     d = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt0, c0, 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[r]), __builtin_amdgcn_exp2f(q[r + 1])};
+    for (int k = 0; k < 16; k += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[k]), __builtin_amdgcn_exp2f(q[k + 1])};
     __builtin_amdgcn_sched_barrier(0);
     q = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt1, c1, 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[r]), __builtin_amdgcn_exp2f(d[r + 1])};
+    for (int k = 0; k < 16; k += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[k]), __builtin_amdgcn_exp2f(d[k + 1])};
   }
 #pragma unroll
-  for (int r = 0; r < 16; r += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[r]), __builtin_amdgcn_exp2f(q[r + 1])};
+  for (int k = 0; k < 16; k += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[k]), __builtin_amdgcn_exp2f(q[k + 1])};
   s[0] += acc0.x + acc0.y;
   s[1] += acc1.x + acc1.y;
 }
@@ -1456,14 +1483,16 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   } else
 #endif
   if (k32) {
-    const float* __restrict__ kq32 = L.P + st.reserved[7];
+    const float* __restrict__ pa = L.P + st.reserved[7] + lane;
     const int h = lane >> 5, n = lane & 31;
     const float v0 = c_p * L.vals[slots[0] * WAVE + n], v1 = c_p * L.vals[slots[0] * WAVE + 32 + n];
     const float bt0 = h ? -1.f : 2.f * v0, bt1 = h ? -1.f : 2.f * v1;
     const float ct0 = -fmaf(v0, v0, 0.f), ct1 = -fmaf(v1, v1, 0.f);
+    const int cbh = cb >> 1, blast = KDE_CHUNKS * cbh - 1;
+    float ring[3] = {pa[0], pa[min(1, blast) * 64], pa[min(2, blast) * 64]};
     for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
       float s2[2] = {0.f, 0.f};
-      kde_mfma32_sums(kq32, ch * (cb >> 1), ch * (cb >> 1) + (cb >> 1), bt0, bt1, ct0, ct1, lane, s2);
+      kde_mfma32_sums(pa, ch * cbh, ch * cbh + cbh, blast, bt0, bt1, ct0, ct1, s2, ring);
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2[0]), __float_as_uint(s2[1]), false, false);
       const float cs = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
       L.scr[ch * WAVE + lane] = cs;
@@ -1472,9 +1501,12 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   } else {
     KdeOps o;
     kde_operands(L, slots, scl, nf, o);
+    const int blast = KDE_CHUNKS * cb - 1;
+    float nx[4];
+    kde_prefetch4(kq, 0, blast, lane, nx);
     for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
       float s[4] = {0.f, 0.f, 0.f, 0.f};
-      kde_sums(kq, ch * cb, ch * cb + cb, o, nf, lane, s);
+      kde_sums(kq, ch * cb, ch * cb + cb, blast, o, nf, lane, s, nx);
       const float cs = kde_reduce_tiles(s, lane);
       L.scr[ch * WAVE + lane] = cs;
       tot += (double)cs;
@@ -1557,14 +1589,18 @@ __device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L,
   {
     KdeOps oy;
     kde_operands(L, slots, scl, dp + D, oy);
-    kde_sums(L.P + st.reserved[2], 0, nb, oy, dp + D, lane, sy4);
+    float nx[4];
+    kde_prefetch4(L.P + st.reserved[2], 0, nb - 1, lane, nx);
+    kde_sums(L.P + st.reserved[2], 0, nb, nb - 1, oy, dp + D, lane, sy4, nx);
   }
   const float sy = kde_reduce_tiles(sy4, lane);
   float sp = 1.f;
   if (!root) {
     KdeOps op;
     kde_operands(L, slots, scl, dp, op);
-    kde_sums(L.P + st.reserved[1], 0, nb, op, dp, lane, sp4);
+    float nx[4];
+    kde_prefetch4(L.P + st.reserved[1], 0, nb - 1, lane, nx);
+    kde_sums(L.P + st.reserved[1], 0, nb, nb - 1, op, dp, lane, sp4, nx);
     sp = kde_reduce_tiles(sp4, lane);
   }
   wave_sync();

@@ -17,7 +17,8 @@ peer sends its shard over its own link to ``dst``, straight into one preallocate
 ``[world, shard, ...]`` buffer whose view is the batch).  ``overlap=True`` issues the gather
 asynchronously so that it runs on RCCL's stream while the next call's walk computes; the
 returned tensors are then valid after :meth:`ShardedEngine.wait` (as with any
-``async_op`` collective).  The same code runs on ``gloo`` (CPU collectives) for the
+``async_op`` collective).  At most one call's gathers are in flight: the next call's gather
+joins the previous one first (a stream wait on RCCL).  The same code runs on ``gloo`` (CPU collectives) for the
 multi-process tests.
 """
 from __future__ import annotations
@@ -102,6 +103,7 @@ class ShardedEngine:
         self._pending = []
         self.last_seed: Optional[int] = None
         self.gather_bytes = 0           # bytes dst received from its peers over all calls (bench.py)
+        self._calls = 0                 # calls made (tags the pending gathers)
 
     def _device(self):
         backend = dist.get_backend(self.group) if dist.is_initialized() else "gloo"
@@ -131,7 +133,7 @@ class ShardedEngine:
 
     def wait(self) -> None:
         """Order the current stream after every pending (``overlap=True``) gather."""
-        for w in self._pending:
+        for _, w in self._pending:
             w.wait()
         self._pending.clear()
 
@@ -169,13 +171,17 @@ class ShardedEngine:
         if rank == self.dst:
             out = torch.empty((world, q_max) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
             parts = list(out.unbind(0))
+        if self.overlap and self._pending and self._pending[-1][0] != self._calls:
+            # at most one earlier call's gathers in flight: join them before issuing this call's
+            # (RCCL: the current stream waits, the host does not; gloo: the host waits).  Ranks
+            # that never wait() -- every non-destination rank -- pile up no Works, and gloo's
+            # queue of matched async collectives stays one call deep
+            self.wait()
         work = dist.gather(src, parts, dst=self.dst, group=self.group, async_op=self.overlap)
         if rank == self.dst:
             self.gather_bytes += (world - 1) * src.numel() * src.element_size()   # received from peers
         if self.overlap:
-            # callers that never wait() (non-dst ranks) must not pile up finished Works
-            self._pending = [w for w in self._pending if not w.is_completed()]
-            self._pending.append(work)
+            self._pending.append((self._calls, work))
         if rank != self.dst:
             return None
         if n_total == world * q_max:                  # equal shards: the buffer is the batch
@@ -202,6 +208,7 @@ class ShardedEngine:
         rank, world = _world(self.group)
         n_total = infer_batch_size(query.evidence, getattr(query, "do", None))
         self._check(n_total, world)
+        self._calls += 1
         b0, b1 = shard_bounds(n_total, rank, world)
         self._set_base(b0)
         kw = self._shard_kwargs(kwargs, b0, b1, n_total)
@@ -217,6 +224,7 @@ class ShardedEngine:
         rank, world = _world(self.group)
         n_total = infer_batch_size(query.evidence, getattr(query, "do", None))
         self._check(n_total, world)
+        self._calls += 1
         b0, b1 = shard_bounds(n_total, rank, world)
         self._set_base(b0)
         kw = self._shard_kwargs(kwargs, b0, b1, n_total)
