@@ -442,6 +442,7 @@ class QueryPlan:
     slot_of: Dict[str, int]
     kind_mask: int = 63       # CPD kinds the walk evaluates (selects the kernel instantiation;
                               # | 32 non-relu activations, | 512 generic-MLP nodes)
+    order: Optional[List[str]] = None   # the walk order of the steps (a topological order)
     wbuf: int = 0             # floats per LDS weight buffer (max wblk_len over the steps)
     # precompute (precompute_plans): the same walk with VBN_F_PRECOMP steps, the one-query
     # pre-pass walk whose out_x the per-sample ones read, and the one-wave-per-query pre-pass
@@ -464,10 +465,53 @@ def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
     return need
 
 
+def liveness_order(model: BNModel, *, fixed: Sequence[str], logp: Sequence[str], out_nodes: Sequence[str],
+                   params: Sequence[str] = (), skip: Sequence[str] = ()) -> List[str]:
+    """A topological order of the non-skipped nodes that keeps few node values live at once
+    (greedy list scheduling: among the ready nodes, the one whose step frees the most parent
+    columns and holds the fewest new ones; ties in the model's order).  Node values live in LDS
+    slots (build_plan's liveness scan), and a wave's LDS footprint bounds how many waves a CU
+    holds: the 128-node cfg5 DAG peaks at 32 live columns in the model's order, 25 here."""
+    skip_s, fixed_s, logp_s, params_s = set(skip), set(fixed), set(logp), set(params)
+    nodes = [n for n in model.topo if n not in skip_s]
+    rank = {n: i for i, n in enumerate(nodes)}
+    reads = {n: (n not in fixed_s) or (n in logp_s) or (n in params_s) for n in nodes}
+    children = {n: [] for n in nodes}
+    for n in nodes:
+        for p in model.parents[n]:
+            if p in rank:
+                children[p].append(n)
+    readers_left = {n: sum(1 for c in children[n] if reads[c]) for n in nodes}
+    waiting = {n: sum(1 for p in model.parents[n] if p in rank) for n in nodes}
+    outs = set(out_nodes)
+    ready = [n for n in nodes if waiting[n] == 0]
+    order: List[str] = []
+    while ready:
+        def cost(n):
+            freed = sum(1 for p in model.parents[n] if p in rank and reads[n] and readers_left[p] == 1
+                        and p not in outs)
+            holds = 0 if (readers_left[n] == 0 and n not in outs) else 1
+            return (holds - freed, rank[n])
+        n = min(ready, key=cost)
+        ready.remove(n)
+        order.append(n)
+        if reads[n]:
+            for p in model.parents[n]:
+                if p in rank:
+                    readers_left[p] -= 1
+        for c in children[n]:
+            waiting[c] -= 1
+            if waiting[c] == 0:
+                ready.append(c)
+    assert len(order) == len(nodes)
+    return order
+
+
 def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[str],
                logp: Sequence[str], out_nodes: Sequence[str], shared_roots: bool, mode: int,
                skip: Sequence[str] = (), exact_f32: bool = False, kde_valu: bool = False,
-               params: Sequence[str] = (), pre_out: Sequence[str] = ()) -> QueryPlan:
+               params: Sequence[str] = (), pre_out: Sequence[str] = (),
+               order: Optional[Sequence[str]] = None) -> QueryPlan:
     """Step table for one query signature.
 
     ``latent``: nodes sampled; ``fixed``: nodes read from the fixed buffer (evidence/do);
@@ -481,13 +525,26 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
     target and CPDHandle.conditional.  ``pre_out``: latent nodes that write their per-sample
     quantities instead of a sample (VBN_F_PRE_OUT, the shared-sample pre-pass of
     :func:`precompute_plans`): NN CPDs their n_out MLP head outputs, KDE its 16 inverse-CDF
-    chunk sums ++ the underflow shift.
+    chunk sums ++ the underflow shift.  ``order``: the walk order of the non-skipped nodes (a
+    topological order; default the model's, reference ``vbn.py:670-675``) -- every draw is keyed
+    by its node, so the order changes only the LDS slot assignment and the Box-Muller pairing
+    (:func:`liveness_order`).
     """
     model = packed.model
     latent_s, fixed_s, logp_s, skip_s = set(latent), set(fixed), set(logp), set(skip)
     params_s = set(params)
     pre_s = set(pre_out)
-    order = [n for n in model.topo if n not in skip_s]
+    if order is None:
+        order = [n for n in model.topo if n not in skip_s]
+    else:
+        order = list(order)
+        if sorted(order) != sorted(n for n in model.topo if n not in skip_s):
+            raise ValueError("order must list every non-skipped node once")
+        seen = set()
+        for n in order:
+            if any(p not in seen and p not in skip_s for p in model.parents[n]):
+                raise ValueError(f"order is not topological at node {n}")
+            seen.add(n)
     for n in order:
         if n in params_s:
             if n in latent_s or n in fixed_s or n in logp_s:
@@ -642,7 +699,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
         steps=steps_t,
         in_cols=t(in_cols), out_cols=t(out_cols), n_steps=len(order), n_slots=max(n_slots, 1),
         max_out=max_out, fixed_nodes=fixed_nodes, fixed_ld=max(c, 1), noise_nodes=noise_nodes,
-        out_nodes=list(out_nodes), mode=mode, slot_of=slot_of, kind_mask=kind_mask,
+        out_nodes=list(out_nodes), mode=mode, slot_of=slot_of, kind_mask=kind_mask, order=list(order),
         wbuf=int(steps[:, S_WBLK_LEN].max()) if len(order) else 0)
 
 
@@ -853,7 +910,7 @@ def precompute_plans(packed: PackedModel, plan: QueryPlan, *, skip: Sequence[str
     """
     model = packed.model
     rows = plan.steps._vbn_host[0].copy()
-    order = [n for n in model.topo if n not in set(skip)]
+    order = list(plan.order) if plan.order is not None else [n for n in model.topo if n not in set(skip)]
     assert len(order) == len(rows)
     at = {n: i for i, n in enumerate(order)}
     roots = [n for n in order if rows[at[n]][S_ROLE] == ROLE_LATENT and rows[at[n]][S_FLAGS] & F_SHARED]
@@ -882,11 +939,11 @@ def precompute_plans(packed: PackedModel, plan: QueryPlan, *, skip: Sequence[str
     pre = pre_q = None
     if cand_s:
         keep = root_s | set(cand_s)
+        porder = [n for n in order if n in keep]         # the main walk's order: its Box-Muller pairs
         pre = build_plan(packed, latent=roots + cand_s, fixed=[], logp=[], out_nodes=cand_s, shared_roots=True,
                          mode=MODE_SAMPLE, skip=[n for n in model.topo if n not in keep], exact_f32=exact_f32,
-                         pre_out=cand_s)
+                         pre_out=cand_s, order=porder)
         prow = pre.steps._vbn_host[0].copy()
-        porder = [n for n in model.topo if n in keep]
         for i, n in enumerate(porder):               # the main walk's Box-Muller pairs (roots pair
             prow[i][S_FLAGS] &= ~(F_BM_FIRST | F_BM_SECOND)        # with roots only) and no others
             if n in root_s:
@@ -897,12 +954,13 @@ def precompute_plans(packed: PackedModel, plan: QueryPlan, *, skip: Sequence[str
         # the candidates writing their quantities (an evidence candidate is one of them)
         cq = set(cand_q)
         keep = fixed_s | cq
+        qorder = [n for n in order if n in keep]
         pre_q = build_plan(packed, latent=cand_q, fixed=[n for n in fixed if n not in cq], logp=[],
                            out_nodes=cand_q, shared_roots=False, mode=MODE_SAMPLE,
-                           skip=[n for n in model.topo if n not in keep], exact_f32=exact_f32, pre_out=cand_q)
+                           skip=[n for n in model.topo if n not in keep], exact_f32=exact_f32, pre_out=cand_q,
+                           order=qorder)
         qrow = pre_q.steps._vbn_host[0].copy()
         qrow[:, S_FLAGS] &= ~(F_BM_FIRST | F_BM_SECOND)          # PRE_OUT steps draw no normals
-        qorder = [n for n in model.topo if n in keep]
         for i, n in enumerate(qorder):
             if n not in cq:
                 qrow[i][S_FIXEDCOL] = rows[at[n]][S_FIXEDCOL]
