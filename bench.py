@@ -356,7 +356,14 @@ def main():
     # (a 20-step window right after a handful of calls measured 0.92 vs 0.82 ms per step in
     # steady state, profiles/r03_bench/r03t_blocks.txt)
     log(f"kernel {kern_ms:.4f} ms; settling calls")
-    for _ in range(max(5, min(200, math.ceil(50.0 / kern_ms)))):
+    n_settle = max(5, min(200, math.ceil(50.0 / kern_ms)))
+    if dist:
+        # every call gathers (a collective): all ranks must make the same number of calls, and
+        # their kernel times differ (the max keeps the slowest rank's ~50 ms)
+        t = torch.tensor([n_settle], dtype=torch.int64, device=device if args.dist_backend == "nccl" else "cpu")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        n_settle = int(t.item())
+    for _ in range(n_settle):
         vbn.infer_posterior(query)
     sharded.wait()
     torch.cuda.synchronize()

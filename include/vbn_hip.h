@@ -34,6 +34,9 @@
  *   vbn_hip_rb_epilogue     the Rao-Blackwellized mixture / categorical marginal of
  *                             RaoBlackwellizedMarginalization.infer_posterior
  *                               (vbn/inference/rao_blackwellized_marginalization.py:255-317)
+ *   vbn_hip_discrete_posterior  the benchmark adapter's discrete weighted histogram
+ *                             _estimate_discrete_posterior[_batch]
+ *                               (benchmarking/models/vbn.py:202-242, _normalize_probs 116-121)
  *   vbn_hip_normalize_weights  torch.softmax(log_weights, 1) + ESS
  *                               (importance_sampling.py:82-84) and the normalize / max-shift
  *                               branch of likelihood_weighting.py:75-80.
@@ -47,7 +50,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 9
+#define VBN_ABI_VERSION 10
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001
@@ -109,6 +112,18 @@ int vbn_hip_resample(const float* w, const float* u, uint64_t seed, uint64_t off
  *   ess[b] = 1 / max(sum_s w^2, eps).   pdf [B][S], x [B][S][D] contiguous. */
 int vbn_hip_posterior_stats(const float* pdf, const float* x, float* mean, float* std, float* ess,
                             int64_t n_queries, int32_t n_samples, int32_t dim, float eps, void* stream);
+
+/* (ABI v10) Discrete weighted histogram per query (benchmarking/models/vbn.py:202-242):
+ *   for s in order: skip a non-finite w[b][s]; i = rint(x[b][s]) (half to even); skip i
+ *   outside [0, k); bins[i] += (double)w[b][s]  (float64 running sums, the reference's order);
+ *   probs[b][c] = bins[c] / total with total = numpy's pairwise sum of the bins, or 1/k each
+ *   when total is not finite or <= 0 (_normalize_probs, vbn.py:116-121).
+ *   bad[b] = 0, or 1 / 2 when a finite-weight sample is NaN / +-inf (the reference raises
+ *   ValueError / OverflowError there; that query's probs are then not meaningful).
+ *   x: sample s of query b at x[(b * n_samples + s) * x_stride] (x_stride = D of a [B][S][D]
+ *   tensor: feature 0); w [B][S]; probs [B][k] float64; bad [B] int32. */
+int vbn_hip_discrete_posterior(const float* x, int64_t x_stride, const float* w, double* probs, int32_t* bad,
+                               int64_t n_queries, int32_t n_samples, int32_t k, void* stream);
 
 /* Rao-Blackwellized target epilogue over P particles per query
  * (rao_blackwellized_marginalization.py:68-76, 255-317):

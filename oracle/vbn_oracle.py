@@ -886,6 +886,56 @@ def posterior_stats(pdf: torch.Tensor, samples: torch.Tensor, eps: float = 1e-12
 
 
 # ----------------------------------------------------------------------------------------
+# discrete weighted histogram (reference benchmarking/models/vbn.py:116-121, 202-242)
+# ----------------------------------------------------------------------------------------
+
+def _normalize_probs_hist(hist) -> List[float]:
+    """_normalize_probs (benchmarking/models/vbn.py:116-121)."""
+    import numpy as np
+    arr = np.asarray(list(hist), dtype=float)
+    total = float(arr.sum())
+    if not math.isfinite(total) or total <= 0:
+        return (np.ones_like(arr) / len(arr)).tolist()
+    return (arr / total).tolist()
+
+
+def estimate_discrete_posterior(samples: torch.Tensor, weights: torch.Tensor, k: int) -> List[float]:
+    """_estimate_discrete_posterior (benchmarking/models/vbn.py:202-223): float64 bins filled
+    in sample order, round half to even, non-finite weights and out-of-range bins skipped."""
+    import numpy as np
+    if samples.dim() == 3:                                               # 207-208
+        samples = samples[:, :, 0]
+    if samples.dim() == 2:                                               # 209-210
+        samples = samples[0]
+    if weights.dim() == 2:                                               # 211-212
+        weights = weights[0]
+    vals = samples.detach().cpu().numpy().reshape(-1)                    # 213-214
+    wts = weights.detach().cpu().numpy().reshape(-1)
+    hist = np.zeros(int(k), dtype=float)                                 # 215
+    for value, weight in zip(vals, wts):                                 # 216-222
+        if not math.isfinite(weight):
+            continue
+        idx = int(round(float(value)))
+        if idx < 0 or idx >= k:
+            continue
+        hist[idx] += float(weight)
+    return _normalize_probs_hist(hist)                                   # 223
+
+
+def estimate_discrete_posterior_batch(samples: torch.Tensor, weights: torch.Tensor, k: int) -> List[List[float]]:
+    """_estimate_discrete_posterior_batch (benchmarking/models/vbn.py:226-242)."""
+    if samples.dim() == 3:
+        samples = samples[:, :, 0]
+    if samples.dim() != 2:
+        raise ValueError(f"Expected samples with 2D shape, got {tuple(samples.shape)}")
+    if weights.dim() != 2:
+        raise ValueError(f"Expected weights with 2D shape, got {tuple(weights.shape)}")
+    if samples.shape[0] != weights.shape[0]:
+        raise ValueError("Samples/weights batch size mismatch")
+    return [estimate_discrete_posterior(samples[i], weights[i], k) for i in range(samples.shape[0])]
+
+
+# ----------------------------------------------------------------------------------------
 # Gibbs sampler (reference vbn/sampling/gibbs.py)
 # ----------------------------------------------------------------------------------------
 

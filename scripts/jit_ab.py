@@ -30,7 +30,8 @@ def main():
     from vectorizedbayesiannetwork_amd import engines as E
 
     torch.cuda.set_device(0)
-    E.PRECOMPUTE = False             # the variants are compiled from the plain plan (jit_variants.py)
+    E.PRECOMPUTE = False             # the variants are compiled from the plain plan (jit_variants.py),
+    E.LIVENESS_ORDER = False         # in the model's order: the launch must carry the same table
     cfg, model, vbn, query = build_workload(a.config, "cuda:0", 1)
     B, S = cfg["B"], cfg["S"]
     vbn.set_inference_method(cfg["engine"], n_samples=S, plan_jit=False)
@@ -79,6 +80,7 @@ def main():
     variants = ["interp"] + list(mods)
     res = {v: [] for v in variants}
     for rnd in range(2):
+        print(f"round {rnd}", file=sys.stderr, flush=True)
         for v in variants:
             stream = torch.cuda.current_stream()
             for rep in range(5):

@@ -25,7 +25,9 @@ ENGINES = {"mcm": "monte_carlo_marginalization", "is": "importance_sampling", "l
 
 def plans_for(name):
     """``cfg`` (the bench engine) or ``cfg:engine`` (mcm / is / lw / ancestral: the engines'
-    plans for the GPU tests' workloads, which share the bench configs' DAGs)."""
+    plans for the GPU tests' workloads, which share the bench configs' DAGs).  Built through
+    the engines' own ``engines._plan`` with their arguments (walk order and precompute
+    included), so the step tables and cache keys are the engines'."""
     import bench
     from vectorizedbayesiannetwork_amd import engines as E
     from vectorizedbayesiannetwork_amd import plan as P
@@ -35,29 +37,24 @@ def plans_for(name):
     vals = set(ev)
     fixed = [x for x in model.topo if x in vals]
     latent = [x for x in model.topo if x not in vals]
+    logp_ev = [x for x in model.topo if x in ev]
     eng = ENGINES[eng_name] if eng_name else cfg["engine"]
-    if eng == "likelihood_weighting":
-        plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[x for x in model.topo if x in vals],
-                            out_nodes=[target], shared_roots=True, mode=P.MODE_WEIGHTED, skip=[])
-        pc = P.precompute_plans(pk, plan, per_query=E.PRECOMPUTE_Q)
-        return cfg, [("plain", plan, False)] + ([("precompute", pc[0], pc[1] is not None)] if pc else [])
-    if eng == "ancestral":
-        plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[], out_nodes=[target], shared_roots=True,
-                            mode=P.MODE_SAMPLE, skip=[])
-        pc = P.precompute_plans(pk, plan, per_query=E.PRECOMPUTE_Q)
-        return cfg, [("plain", plan, False)] + ([("precompute", pc[0], pc[1] is not None)] if pc else [])
-    if eng == "importance_sampling":
-        plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[x for x in model.topo if x in vals],
-                            out_nodes=[target], shared_roots=False, mode=P.MODE_WEIGHTED, skip=[])
+    common = dict(latent=latent, fixed=fixed, out_nodes=[target], skip=[], exact_f32=False, kde_valu=False)
+    if eng in ("likelihood_weighting", "importance_sampling"):
+        lw = eng == "likelihood_weighting"
+        key = ("weighted", target, tuple(sorted(ev)), (), lw, False, False, False)
+        plan = E._plan(pk, key, logp=logp_ev, shared_roots=lw, mode=P.MODE_WEIGHTED, **common)
+    elif eng == "ancestral":
+        key = ("ancestral", target, tuple(sorted(vals)), False, False, False)
+        plan = E._plan(pk, key, logp=[], shared_roots=True, mode=P.MODE_SAMPLE, **common)
     elif eng == "monte_carlo_marginalization":
-        plan = P.build_plan(pk, latent=latent, fixed=fixed, logp=[target], out_nodes=[target],
-                            shared_roots=True, mode=P.MODE_MCM, skip=[])
+        key = ("mcm", target, tuple(sorted(vals)), False, False, False)
+        plan = E._plan(pk, key, logp=[target], shared_roots=True, mode=P.MODE_MCM, **common)
     else:
         return cfg, []
     out = [("plain", plan, False)]
-    pc = P.precompute_plans(pk, plan, per_query=E.PRECOMPUTE_Q)
-    if pc is not None:
-        out.append(("precompute", pc[0], pc[1] is not None))
+    if plan.pc is not None:
+        out.append(("precompute", plan.pc, plan.pre is not None))
     return cfg, out
 
 

@@ -12,7 +12,8 @@ the reference op sequence on the kernel's own random numbers:
   every query (root nodes of MCM / LW / ancestral, SURVEY Q5), else ``q_base + query + 1``;
 * stream 0: a standard normal by Box-Muller on both words, ``r cos(2 pi u2)``; in lean walks
   a ``VBN_F_BM_FIRST`` step also yields ``r sin(2 pi u2)`` for the next ``VBN_F_BM_SECOND``
-  step's dim-0 normal (plan.py ``_pair_normals``);
+  step's dim-0 normal in the walk's order (plan.py ``_pair_normals``; the walk order may
+  differ from the oracle's topological call order, plan.liveness_order);
 * stream 1: two uniforms ``(w >> 8) * 2^-24``: word 0 picks the categorical / KDE index
   (inverse CDF: the smallest k with cumsum(p)[k] > u * sum(p)), word 1 is softmax_nn's
   within-bin uniform.
@@ -75,6 +76,15 @@ class PhiloxDraws:
                  n_queries: int, n_samples: int, lean: bool = True):
         rows = steps.detach().cpu().numpy() if isinstance(steps, torch.Tensor) else np.asarray(steps)
         self.row_of = {int(r[S_NODEID]): r for r in rows}
+        # a VBN_F_BM_SECOND step takes r sin of the nearest VBN_F_BM_FIRST step before it in the
+        # walk's order (plan._pair_normals), whatever order the oracle calls the nodes in
+        self.partner = {}
+        first = None
+        for r in rows:
+            if int(r[S_FLAGS]) & F_BM_FIRST:
+                first = r
+            elif int(r[S_FLAGS]) & F_BM_SECOND:
+                self.partner[int(r[S_NODEID])] = first
         self.node_ids = dict(node_ids)
         self.seed = int(seed) & ((1 << 64) - 1)
         self.offset = int(offset)
@@ -82,7 +92,6 @@ class PhiloxDraws:
         self.B = int(n_queries)
         self.S = int(n_samples)
         self.lean = bool(lean)
-        self.spare = np.zeros((self.B, self.S), np.float32)
         self.margin = np.full((self.B, self.S), np.inf)
         self.n_categorical = 0
         self._row = None
@@ -112,12 +121,13 @@ class PhiloxDraws:
         q = qi + (self._query or 0)
         return q, s, d
 
-    def _words(self, q, s, d, stream: int):
+    def _words(self, q, s, d, stream: int, row=None):
         if self._row is None:
             raise RuntimeError("PhiloxDraws: draw before begin_node")
-        node_id = int(self._row[S_NODEID])
+        row = self._row if row is None else row
+        node_id = int(row[S_NODEID])
         sid = ((self.offset & 0xFF) << 24) | (node_id << 10) | (np.asarray(d, np.int64) << 2) | stream
-        qkey = np.zeros_like(q) if self._shared else (self.q_base + q + 1)
+        qkey = np.zeros_like(q) if (int(row[S_FLAGS]) & F_SHARED) else (self.q_base + q + 1)
         c1 = (qkey.astype(np.uint64) & MASK32) ^ np.uint64((self.seed >> 32) & 0xFFFFFFFF)
         key = (np.uint64(self.seed & 0xFFFFFFFF) + sid.astype(np.uint64)) & MASK32
         return philox2x32(s, c1, key)
@@ -158,15 +168,10 @@ class PhiloxDraws:
         cos, sin = box_muller_pair(a, b)
         out = cos.copy()
         fl = int(self._row[S_FLAGS])
-        if self.lean and (fl & (F_BM_FIRST | F_BM_SECOND)):
+        if self.lean and (fl & F_BM_SECOND):
             d0 = d == 0
-            if fl & F_BM_SECOND:
-                out[d0] = self.spare[q[d0], s[d0]]
-            else:
-                if self._shared:
-                    self.spare[:, s[d0]] = sin[d0][None, :]
-                else:
-                    self.spare[q[d0], s[d0]] = sin[d0]
+            pa, pb = self._words(q[d0], s[d0], d[d0], 0, row=self.partner[int(self._row[S_NODEID])])
+            out[d0] = box_muller_pair(pa, pb)[1]
         return torch.from_numpy(out.reshape(shape))
 
     def uniform(self, shape) -> torch.Tensor:               # softmax_nn within-bin uniform

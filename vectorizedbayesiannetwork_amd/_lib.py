@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -23,6 +23,7 @@ EXPORTS = (
     "vbn_hip_rb_epilogue",
     "vbn_hip_resample",
     "vbn_hip_posterior_stats",
+    "vbn_hip_discrete_posterior",
     "vbn_hip_lds_bytes",
     "vbn_hip_struct_size",
     "vbn_hip_walk_kind_set",
@@ -119,6 +120,10 @@ def load(path: str = None) -> ctypes.CDLL:
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
         lib.vbn_hip_posterior_stats.restype = ctypes.c_int
+        lib.vbn_hip_discrete_posterior.argtypes = [
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+        lib.vbn_hip_discrete_posterior.restype = ctypes.c_int
         lib.vbn_hip_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
         lib.vbn_hip_lds_bytes.restype = ctypes.c_int64
         lib.vbn_hip_walk_kind_set.argtypes = [ctypes.POINTER(VbnWalkArgs)]

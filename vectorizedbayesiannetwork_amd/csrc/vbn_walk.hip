@@ -285,6 +285,82 @@ __global__ void __launch_bounds__(RB_THREADS) vbn_posterior_stats_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// discrete weighted histogram of a target's samples (benchmarking/models/vbn.py:202-242,
+// _estimate_discrete_posterior[_batch]): one lane per query walks its S (sample, weight) pairs
+// in order -- the reference's float64 running sums, so the bins are bit-identical -- skipping
+// non-finite weights and indices rint(x) outside [0, k); then _normalize_probs (vbn.py:116-121):
+// total = numpy's pairwise sum of the bins (add.reduce from the identity 0.0), probs = bins /
+// total, or 1/k each when total is not finite or <= 0.  A finite weight whose sample is NaN /
+// +-inf is the reference's ValueError / OverflowError (int(round(x))): bad[b] records the first
+// one (1 NaN, 2 inf) and the query's row is not meaningful.  Bins live in LDS ([k][64] doubles,
+// k <= 128) or, for more bins, in the output row itself.
+// ------------------------------------------------------------------------------------------
+#define DP_THREADS 64
+#define DP_LDS_BINS 128
+
+// numpy pairwise_sum (umath loops_utils.h): n < 8 sequential from 0.0; n <= 128 eight strided
+// accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus the tail; else split at
+// n/2 rounded down to a multiple of 8.  D bounds the split depth at compile time (no recursion).
+template <int D>
+__device__ double np_pairwise_sum(const double* a, int64_t n, int64_t st) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int64_t i = 0; i < n; ++i) r += a[i * st];
+    return r;
+  }
+  if (n <= 128 || D == 0) {
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = a[j * st];
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] += a[(i + j) * st];
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i * st];
+    return res;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  return np_pairwise_sum<(D > 0 ? D - 1 : 0)>(a, n2, st) + np_pairwise_sum<(D > 0 ? D - 1 : 0)>(a + n2 * st, n - n2, st);
+}
+
+template <bool LDS_BINS>
+__global__ void __launch_bounds__(DP_THREADS) vbn_discrete_posterior_kernel(
+    const float* __restrict__ x, int64_t x_stride, const float* __restrict__ w, double* __restrict__ probs,
+    int32_t* __restrict__ bad, int64_t B, int S, int k) {
+#pragma clang fp contract(off)
+  extern __shared__ double bins_lds[];
+  const int64_t b = (int64_t)blockIdx.x * DP_THREADS + threadIdx.x;
+  if (b >= B) return;                                    // no barriers below
+  double* h = LDS_BINS ? bins_lds + threadIdx.x : probs + b * k;
+  const int64_t hs = LDS_BINS ? DP_THREADS : 1;
+  for (int c = 0; c < k; ++c) h[c * hs] = 0.0;
+  const float* xr = x + b * (int64_t)S * x_stride;
+  const float* wr = w + b * (int64_t)S;
+  int flag = 0;
+  for (int s = 0; s < S; ++s) {
+    const float wt = wr[s];
+    if (!__builtin_isfinite(wt)) continue;
+    const float v = xr[(int64_t)s * x_stride];
+    if (!__builtin_isfinite(v)) {
+      flag = v != v ? 1 : 2;
+      break;
+    }
+    const double r = __builtin_rint((double)v);        // round half to even, as Python's round
+    if (r < 0.0 || r >= (double)k) continue;
+    h[(int64_t)r * hs] += (double)wt;
+  }
+  bad[b] = flag;
+  const double total = 0.0 + np_pairwise_sum<24>(h, k, hs);
+  const bool ok = __builtin_isfinite(total) && total > 0.0;
+  const double uni = 1.0 / (double)k;
+  double* out = probs + b * k;
+  for (int c = 0; c < k; ++c) out[c] = ok ? h[c * hs] / total : uni;
+}
+
+// ------------------------------------------------------------------------------------------
 // C-ABI
 // ------------------------------------------------------------------------------------------
 static thread_local char g_err[512];
@@ -512,6 +588,24 @@ extern "C" int vbn_hip_posterior_stats(const float* pdf, const float* x, float* 
     return fail(VBN_E_ARGS, "vbn_hip_posterior_stats: bad arguments");
   hipLaunchKernelGGL(vbn_posterior_stats_kernel, dim3((unsigned)n_queries), dim3(RB_THREADS), 0,
                      (hipStream_t)stream, pdf, x, mean, std, ess, n_samples, dim, eps);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  return 0;
+}
+
+extern "C" int vbn_hip_discrete_posterior(const float* x, int64_t x_stride, const float* w, double* probs,
+                                          int32_t* bad, int64_t n_queries, int32_t n_samples, int32_t k,
+                                          void* stream) {
+  if (!x || !w || !probs || !bad || x_stride <= 0 || n_queries <= 0 || n_samples <= 0 || k <= 0)
+    return fail(VBN_E_ARGS, "vbn_hip_discrete_posterior: bad arguments");
+  const unsigned grid = (unsigned)((n_queries + DP_THREADS - 1) / DP_THREADS);
+  if (k <= DP_LDS_BINS)
+    hipLaunchKernelGGL(vbn_discrete_posterior_kernel<true>, dim3(grid), dim3(DP_THREADS),
+                       (size_t)k * DP_THREADS * sizeof(double), (hipStream_t)stream, x, x_stride, w, probs, bad,
+                       n_queries, n_samples, k);
+  else
+    hipLaunchKernelGGL(vbn_discrete_posterior_kernel<false>, dim3(grid), dim3(DP_THREADS), 0, (hipStream_t)stream,
+                       x, x_stride, w, probs, bad, n_queries, n_samples, k);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;

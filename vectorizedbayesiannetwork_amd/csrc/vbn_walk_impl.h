@@ -1307,11 +1307,17 @@ __device__ __forceinline__ float kde_reduce_tiles(const float (&s)[4], int lane)
 // walk different nodes, so most operand loads are served by the Infinity Cache (cfg4: 78 GB
 // of L2 fills per launch, r04 PMC), ~545+ cycles away -- more than one block of work covers.
 
+#ifdef VBN_ABL_L2FIT
+#define KDE_BLK(x) ((x) & 31)        // ablation: every pass re-reads its node's first 32 blocks
+#else
+#define KDE_BLK(x) (x)
+#endif
+
 // first four 16-point blocks of a pass over pack kq starting at block b0 (blast = last block)
 __device__ __forceinline__ void kde_prefetch4(const float* __restrict__ kq, int b0, int blast, int lane,
                                               float (&nx)[4]) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) nx[u] = kq[min(b0 + u, blast) * 64 + lane];
+  for (int u = 0; u < 4; ++u) nx[u] = kq[KDE_BLK(min(b0 + u, blast)) * 64 + lane];
 }
 
 // per-lane partial sums of exp2(arg) over 16-point blocks [b0, b1) of pack kq, b1 - b0 a
@@ -1331,7 +1337,7 @@ __device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int 
   for (int b = b0; b < b1; b += 4) {
     const float a[4] = {nx[0], nx[1], nx[2], nx[3]};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) nx[u] = kq[min(b + 4 + u, blast) * 64 + lane];   // next trip's operands
+    for (int u = 0; u < 4; ++u) nx[u] = kq[KDE_BLK(min(b + 4 + u, blast)) * 64 + lane];   // next trip's operands
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       f32x4 d[4];
@@ -1375,7 +1381,7 @@ __device__ __forceinline__ void kde_mfma32_sums(const float* __restrict__ pa, in
     const float a = r[0];
     r[0] = r[1];
     r[1] = r[2];
-    r[2] = pa[min(i + 3, blast) * 64];
+    r[2] = pa[KDE_BLK(min(i + 3, blast)) * 64];
     return a;
   };
   // software pipeline: the exps of one MFMA run while the next MFMA is in the matrix pipe

@@ -43,7 +43,7 @@ import torch
 from . import ops
 from .model import BNModel, model_from_vbn
 from .plan import (MODE_MCM, MODE_SAMPLE, MODE_WEIGHTED, GibbsPlan, PackedModel, QueryPlan, barren_pruned,
-                   precompute_plans,
+                   liveness_order, precompute_plans,
                    build_gibbs_plan, build_plan)
 from .registry import register_inference, register_sampling
 
@@ -116,6 +116,15 @@ def _plan(pk: PackedModel, key, **kw) -> QueryPlan:
     p = pk.model._cache.get(ck)
     if p is None:
         p = build_plan(pk, **kw)
+        if LIVENESS_ORDER and key[0] in _ORDERED and not kw.get("params") and _lds_bound(p):
+            # the wave's LDS (value slots + scratch rows) limits the waves per CU: walk the DAG
+            # in an order that keeps fewer values live (same draws, keyed by node; plan.py
+            # liveness_order) when that frees slots
+            q = build_plan(pk, order=liveness_order(pk.model, fixed=kw.get("fixed", ()), logp=kw.get("logp", ()),
+                                                    out_nodes=kw.get("out_nodes", ()), skip=kw.get("skip", ())),
+                           **kw)
+            if q.n_slots < p.n_slots:
+                p = q
         if not kw.get("params"):
             # nodes whose parents are all shared root draws (once per sample) or all evidence
             # (once per query)
@@ -125,6 +134,18 @@ def _plan(pk: PackedModel, key, **kw) -> QueryPlan:
                 p.pc, p.pre, p.pre_q = pc
         pk.model._cache[ck] = p
     return p
+
+
+# walk orders other than the model's (plan.liveness_order) for these plan kinds when LDS bounds
+# the occupancy; RIS keeps the topological segments, Gibbs its level schedule
+LIVENESS_ORDER = os.environ.get("VBN_LIVENESS_ORDER", "1") != "0"
+_ORDERED = ("mcm", "mcm-short", "weighted", "ancestral")
+WAVES_PER_CU = 16                    # 4 waves per SIMD at the walk's 128-VGPR budget
+
+
+def _lds_bound(p: QueryPlan) -> bool:
+    """the plan's per-wave LDS (vbn_hip_lds_bytes) holds fewer than WAVES_PER_CU waves per CU"""
+    return (p.n_slots + max(p.max_out, 1)) * 64 * 4 * WAVES_PER_CU > 160 * 1024
 
 
 # per-sample / per-query precompute (plan.precompute_plans) in production walks; False: every

@@ -439,6 +439,39 @@ def _posterior_stats_fake(pdf, samples, eps):
     return pdf.new_empty(b, d), pdf.new_empty(b, d), pdf.new_empty(b)
 
 
+@torch.library.custom_op("vbn_hip::discrete_posterior", mutates_args=())
+def discrete_posterior(samples: Tensor, weights: Tensor, k: int) -> Tuple[Tensor, Tensor]:
+    """samples [B,S] or [B,S,D] (feature 0), weights [B,S], k bins -> (probs [B,k] float64,
+    bad [B] int32) (benchmarking/models/vbn.py:202-242; bad: 1 / 2 where a finite-weight sample
+    is NaN / +-inf, which the reference raises on)."""
+    if weights.device.type != "cuda" or weights.dim() != 2 or samples.dim() not in (2, 3):
+        raise ValueError("vbn_hip::discrete_posterior: samples [B,S(,D)] and weights [B,S] GPU tensors expected")
+    if tuple(samples.shape[:2]) != tuple(weights.shape) or k <= 0:
+        raise ValueError("vbn_hip::discrete_posterior: samples/weights shape mismatch or k <= 0")
+    b, s = weights.shape
+    weights = weights.to(torch.float32).contiguous()
+    samples = samples.to(device=weights.device, dtype=torch.float32).contiguous()
+    stride = samples.shape[2] if samples.dim() == 3 else 1
+    probs = torch.empty(b, k, device=weights.device, dtype=torch.float64)
+    bad = torch.empty(b, device=weights.device, dtype=torch.int32)
+    if b == 0 or s == 0:
+        probs.fill_(1.0 / k)
+        bad.zero_()
+        return probs, bad
+    lib = _lib.load()
+    with torch.cuda.device(weights.device):
+        _lib.check(lib.vbn_hip_discrete_posterior(
+            _ptr(samples), stride, _ptr(weights), _ptr(probs), _ptr(bad), b, s, int(k),
+            ctypes.c_void_p(_stream_handle(weights.device))), "vbn_hip_discrete_posterior")
+    return probs, bad
+
+
+@discrete_posterior.register_fake
+def _discrete_posterior_fake(samples, weights, k):
+    b = weights.shape[0]
+    return weights.new_empty(b, k, dtype=torch.float64), weights.new_empty(b, dtype=torch.int32)
+
+
 # ------------------------------------------------------------------------------------------
 # Query-level ops (SURVEY §8(b)): a packed plan + evidence in, the engine's outputs out.
 #
