@@ -22,3 +22,7 @@ grep variant gpurun_out/r04g_ab_cfg4.txt
 VBN_LIVENESS_ORDER=0 timeout -k 10 300 python -u scripts/jit_ab.py --config cfg3 abx/plan_cfg3_base.hsaco abx/plan_cfg3_wpe3.hsaco \
   > gpurun_out/r04g_ab_cfg3.txt 2>&1 || exit 1
 grep variant gpurun_out/r04g_ab_cfg3.txt
+timeout -k 10 300 python -u scripts/gen_ab.py --config cfg4 --gens 1 4 8 16 32 > gpurun_out/r04g_gen_cfg4.txt 2>&1 || exit 1
+cat gpurun_out/r04g_gen_cfg4.txt
+timeout -k 10 300 python -u scripts/gen_ab.py --config cfg5 --gens 1 4 8 16 32 > gpurun_out/r04g_gen_cfg5.txt 2>&1 || exit 1
+cat gpurun_out/r04g_gen_cfg5.txt
