@@ -95,8 +95,10 @@ enum vbn_mode {
  * split-f16 W2 | W3 | b3], rounded up to a multiple of 256 floats (params float offset,
  * length in floats), which the walk stages into LDS one step ahead (0 = the step runs no
  * MLP); the exact-f32 W2 copy (off_w2) deliberately stays outside the block and is read from
- * global memory on the rare exact path; [7] = one-feature KDE point pack in the
- * v_mfma_f32_32x32x2_f32 operand layout ([rows/32][2][32]: scaled point, |point|^2), or -1. */
+ * global memory on the rare exact path; [7] unused (-1).  KDE packs [1] (parent features) and
+ * [2] (parent ++ target features) hold the bf16x3 slots of v_mfma_f32_16x16x32_bf16
+ * ([block][quarter][16 points][8 bf16], plan.py _kde_pack_bf16); [3] = per-point f32 records,
+ * [4] = the packed-VALU layout. */
 typedef struct vbn_step {
   int32_t kind, role, flags, act;
   int32_t n_in, in_off, out_col, out_dim;

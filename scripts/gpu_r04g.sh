@@ -4,7 +4,7 @@
 # ablations of cfg5 and cfg4 (A/B code objects compiled from the default-order plans)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_histogram.py tests/test_abi.py -v --timeout 120 \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_histogram.py tests/test_abi.py tests/test_gpu_generations.py -v --timeout 120 \
   --timeout-method thread -p no:cacheprovider > gpurun_out/r04g_hist.txt 2>&1 || { tail -30 gpurun_out/r04g_hist.txt; exit 1; }
 tail -2 gpurun_out/r04g_hist.txt
 bash scripts/gpu_r04e.sh || exit 1

@@ -321,31 +321,61 @@ def test_kde_mfma_pack_gives_kernel_weights(nf):
     assert (w[:, m:] == 0).all()
 
 
-def test_kde_pack32_gives_kernel_weights():
-    """The one-feature 32x32x2 pack (plan._kde_pack32) in the v_mfma_f32_32x32x2_f32 operand
-    layout (A[m = l & 31][k = l >> 5] from pack[block][k][32]; B = (2x', -1); C = -|x'|^2,
-    k-ordered fmaf chain from C as csrc kde_arg_rec(nf < 0) replicates it) gives
-    exp2(d) = exp(-|x - y|^2 / (2 s^2)); padding points weigh 0; chunk rows match _kde_pack."""
-    from vectorizedbayesiannetwork_amd.plan import _KDE_C, _kde_cb, _kde_pack, _kde_pack32, KDE_CHUNKS
-    rng = np.random.default_rng(5)
+@pytest.mark.parametrize("nf", [1, 2, 3])
+def test_kde_bf16_pack_gives_kernel_weights(nf):
+    """The bf16x3 point pack (plan._kde_pack_bf16) in the v_mfma_f32_16x16x32_bf16 operand layout
+    (lane l: A = point l & 15's slots 8 (l >> 4) .. +7; B = the particle's slots, csrc
+    kde_bf16_ops: 2x' split into bf16 hi / mid / lo in the _BF16_B pattern, -1 against |y'|^2's
+    split, the split of -|x'|^2 against 1.0; C = 0) gives, with exact bf16 products summed in
+    float64, -|x' - y'|^2 to float32 accuracy (the float32 contraction's rounding, as the 16x16x4
+    form): exp2 of it = exp(-|x - y|^2 / (2 s^2)) within 1e-5 (the f32 inputs' rounding);
+    padding points weigh 0; the three-way splits are exact."""
+    from vectorizedbayesiannetwork_amd.plan import (_BF16_B, _KDE_C, _bf16_split3, _kde_cb, _kde_pack,
+                                                    _kde_pack_bf16, KDE_BF16_K, KDE_CHUNKS)
+    rng = np.random.default_rng(10 + nf)
     m, s = 77, 0.6
     c = np.float32(_KDE_C / s)
-    pts = rng.normal(size=(m, 1)).astype(np.float32)
-    parts = rng.normal(size=(64, 1)).astype(np.float32)
-    pk = _kde_pack32(pts * c)
+    pts = rng.normal(size=(m, nf)).astype(np.float32) * 2
+    parts = rng.normal(size=(64, nf)).astype(np.float32) * 2
+    v = (rng.normal(size=1000) * 10.0 ** rng.integers(-6, 6, 1000)).astype(np.float32)
+    bits = [(h.astype(np.uint32) << 16).view(np.float32).astype(np.float64) for h in _bf16_split3(v)]
+    assert np.array_equal(bits[0] + bits[1] + bits[2], v.astype(np.float64))
+
+    def f64(h):
+        return (np.asarray(h).astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    pk = _kde_pack_bf16(pts * c).view(np.uint16)
     rows = KDE_CHUNKS * _kde_cb(m) * 16
-    assert pk.shape == (rows // 32, 2, 32) and _kde_pack([pts * c]).shape[0] * 16 == rows
-    x = (parts * c)[:, 0].astype(np.float32)
+    assert _kde_pack([pts * c]).shape[0] * 16 == rows and pk.size == rows * KDE_BF16_K
+    lanes = pk.reshape(rows // 16, 64, 8)                      # lane l of block b reads lanes[b, l]
+    a = np.zeros((rows, KDE_BF16_K))
+    for l in range(64):
+        a[np.arange(rows // 16) * 16 + (l & 15), 8 * (l >> 4): 8 * (l >> 4) + 8] = f64(lanes[:, l])
+    x = (parts * c).astype(np.float32)
     w = np.zeros((64, rows))
-    for b in range(rows // 32):
-        a = pk[b].reshape(-1)                                    # lane l reads a[l]
-        for p in range(64):
-            negsq = np.float32(-np.float32(x[p] * x[p]))
-            for r in range(32):
-                d = np.float32(np.float32(a[r] * np.float32(2 * x[p])) + negsq)
-                d = np.float32(d - a[32 + r])
-                w[p, b * 32 + r] = 2.0 ** float(d)
-    ref = np.exp(-0.5 * ((parts[:, None, 0].astype(np.float64) - pts[None, :, 0]) ** 2) / s ** 2)
+    for p in range(64):
+        u = (2 * x[p]).astype(np.float32)
+        sq = np.float32(0)
+        for f in range(nf):
+            sq = np.float32(sq + np.float32(x[p, f] * x[p, f]))
+        b = np.zeros(KDE_BF16_K)
+        for f in range(nf):
+            sp = [f64(h)[0] for h in _bf16_split3(np.array([u[f]], np.float32))]
+            for j in range(6):
+                b[6 * f + j] = sp[_BF16_B[j]]
+        b[18:21] = -1.0
+        b[21:24] = [f64(h)[0] for h in _bf16_split3(np.array([-sq], np.float32))]
+        d = a @ b
+        w[p] = np.exp2(d)
+        # the float32 form of the same contraction (csrc kde_arg_rec, the pass-2 replica)
+        yq = (pts * c).astype(np.float32)
+        ysq = (yq.astype(np.float64) ** 2).sum(1).astype(np.float32)
+        d32 = np.full(m, -sq, np.float32)
+        for f in range(nf):
+            d32 = (d32 + u[f] * yq[:, f]).astype(np.float32)
+        d32 = (d32 - ysq).astype(np.float32)
+        scale = np.abs(2 * x[p] @ yq.T) + ysq + sq
+        assert (np.abs(d[:m] - d32) <= 4e-7 * scale + 1e-30).all()
+    ref = np.exp(-0.5 * ((parts[:, None, :].astype(np.float64) - pts[None].astype(np.float64)) ** 2).sum(-1) / s ** 2)
     np.testing.assert_allclose(w[:, :m], ref, rtol=1e-5, atol=1e-30)
     assert (w[:, m:] == 0).all()
 

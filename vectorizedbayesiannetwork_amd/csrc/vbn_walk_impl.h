@@ -1220,39 +1220,14 @@ __device__ __forceinline__ float kde_qy(const float* __restrict__ pty, float x0,
 // The kernel weight of particle n and stored point m is exp(-|x_n - y_m|^2 / (2 s^2)) =
 // exp2(-|x'_n - y'_m|^2) with x' = c x, y' = c y, c = sqrt(log2(e) / 2) / s, and
 //   -|x' - y'|^2 = sum_k (2 x'_k) y'_k - |y'|^2 - |x'|^2,
-// a contraction over K <= 4 features: one v_mfma_f32_16x16x4_f32 per 16 points x 16 particles
-// (A = point features, host-packed as [block][k][16]; B = particle features; see KdeOps for
-// the two operand forms).  Padding points have |y'|^2 = 1e30 -> weight 0.  The MFMA is a
-// k-ordered fmaf chain from C, so kde_arg_rec() reproduces any element bit-for-bit on VALU
-// (the inverse-CDF scan).  The wave's 64 particles are 4 tiles of 16 (tile t = particles
-// 16t .. 16t+15); D layout: lane l holds points 4(l>>4) .. +3 of the block for particle
-// 16t + (l&15).  Bound: v_exp_f32 issue (one exp per pair); MFMA pipe 32 cycles per 256 pairs.
-struct KdeOps {
-  float b[4];      // B operand of tile t (feature l>>4 of particle 16t + (l&15))
-  float negsq[4];  // -|x'|^2 of particle 16t + (l&15)
-};
-
-// Two operand forms, chosen by the feature count nf (host packs match, plan.py _kde_pack):
-//   nf <= 2 ("ZC"): K = nf + 2, A = (y'.., |y'|^2, 1), B = (2x'.., -1, -|x'|^2), C = 0
-//   nf == 3       : K = 4,      A = (y'.., |y'|^2),    B = (2x'.., -1),          C = -|x'|^2
-// features: nf (slot, scale) pairs; slot = LDS value column.
-__device__ __forceinline__ void kde_operands(const Lane& L, const int (&slots)[4], const float (&scl)[4],
-                                             int nf, KdeOps& o) {
-  const int g = L.lane >> 4, n = L.lane & 15;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    float sq = 0.f, mine = 0.f;
-    for (int f = 0; f < nf; ++f) {
-      const float v = scl[f] * L.vals[slots[f] * WAVE + 16 * t + n];
-      sq = fmaf(v, v, sq);
-      if (f == g) mine = 2.f * v;
-    }
-    o.b[t] = g < nf ? mine : (g == nf ? -1.f : ((g == nf + 1 && nf <= 2) ? -sq : 0.f));
-    o.negsq[t] = -sq;
-  }
-}
-
-// the lane's own particle: x'_k and -|x'|^2 exactly as kde_operands computes them
+// a contraction over K <= 3 features, computed on bf16 MFMAs from exact three-way splits
+// (kde_bf16_sums below) for the inverse-CDF chunk sums and the log-density sums alike.
+// Padding points have |y'|^2 = 1e30 -> weight 0.  The wave's 64 particles are 4 tiles of 16
+// (tile t = particles 16t .. 16t+15); D layout: lane l holds points 4(l>>4) .. +3 of the block
+// for particle 16t + (l&15).  Bound: v_exp_f32 issue (one exp per pair).  The inverse-CDF scan
+// recomputes its chunk's weights with kde_arg_rec, the float32 chain of the same contraction
+// (equal to the MFMA sums to f32 rounding; a crossing past the chunk end is clamped, kde_scan).
+// the lane's own particle: x'_k and -|x'|^2 exactly as kde_bf16_ops computes them
 __device__ __forceinline__ float kde_own(const Lane& L, const int (&slots)[4], const float (&scl)[4], int nf,
                                          float (&xv)[4]) {
   float sq = 0.f;
@@ -1264,16 +1239,10 @@ __device__ __forceinline__ float kde_own(const Lane& L, const int (&slots)[4], c
   return -sq;
 }
 
-// VALU replica of one MFMA output element (k-ordered fmaf chain from C), point record r =
+// VALU form of one pair's argument (a k-ordered fmaf chain), point record r =
 // (y'_0 .. y'_{nf-1}, |y'|^2, ..) of the per-point record pack.
 __device__ __forceinline__ float kde_arg_rec(const float4 r, float xb0, float xb1, float xb2, float negsq,
                                              int nf) {
-  if (nf < 0) {                       // "C form" of -nf features (32x32x2 MFMA, VALU pass 1)
-    float d = fmaf(r.x, xb0, negsq);
-    if (nf < -1) d = fmaf(r.y, xb1, d);
-    if (nf < -2) d = fmaf(r.z, xb2, d);
-    return fmaf(nf == -1 ? r.y : (nf == -2 ? r.z : r.w), -1.f, d);
-  }
   const bool zc = nf <= 2;
   float d = zc ? 0.f : negsq;
   d = fmaf(r.x, xb0, d);
@@ -1303,9 +1272,10 @@ __device__ __forceinline__ float kde_reduce_tiles(const float (&s)[4], int lane)
 }
 
 // Point operands are prefetched a whole trip ahead, across chunk boundaries: the packs of a
-// 64-node M = 10,000 DAG (~5 MB) do not stay in one XCD's 4 MiB L2 while ~4,000 resident waves
-// walk different nodes, so most operand loads are served by the Infinity Cache (cfg4: 78 GB
-// of L2 fills per launch, r04 PMC), ~545+ cycles away -- more than one block of work covers.
+// 64-node M = 10,000 DAG do not stay in one XCD's 4 MiB L2 while ~4,000 resident waves walk
+// different nodes, so most operand loads are served by the Infinity Cache (cfg4: 78 GB of L2
+// fills per launch, r04 PMC), ~545+ cycles away.  Measured not to cost time: re-reading only
+// the first 32 blocks of every pack (VBN_ABL_L2FIT, L2-resident) ran 202.5 vs 201.0 ms.
 
 #ifdef VBN_ABL_L2FIT
 #define KDE_BLK(x) ((x) & 31)        // ablation: every pass re-reads its node's first 32 blocks
@@ -1313,36 +1283,89 @@ __device__ __forceinline__ float kde_reduce_tiles(const float (&s)[4], int lane)
 #define KDE_BLK(x) (x)
 #endif
 
-// first four 16-point blocks of a pass over pack kq starting at block b0 (blast = last block)
-__device__ __forceinline__ void kde_prefetch4(const float* __restrict__ kq, int b0, int blast, int lane,
-                                              float (&nx)[4]) {
-#pragma unroll
-  for (int u = 0; u < 4; ++u) nx[u] = kq[KDE_BLK(min(b0 + u, blast)) * 64 + lane];
+// Pass-1 sums on v_mfma_f32_16x16x32_bf16 ("bf16x3"): rows = 16 points, columns = the 16
+// particles of tile t, K = 32 slots.  Every f32 operand is split into three bf16 whose sum is
+// it exactly (hi = bf16(v), mid = bf16(v - hi), lo = the 8-bit rest); per feature the six
+// products u_h y_h, u_h y_m, u_m y_h, u_h y_l, u_l y_h, u_m y_m (u = 2x' on the B side, y' on
+// the A side; the omitted terms are < 2^-25 of u y) are exact in f32, |y'|^2's three parts meet
+// -1 and 1.0 meets -|x'|^2's three parts, so the MFMA's f32 sum from C = 0 is the 16x16x4
+// form's contraction to f32 rounding (tests/test_plan.py).  One bf16 MFMA per tile and 16
+// points -- 16 cycles of the matrix pipe per 256 pairs, which the 16 exps per lane it feeds
+// hide -- against the f32 16x16x4 MFMA's 32 cycles, during which VALU issue also stalls
+// (profiles/microbench/coissue_sgb_r03.json).  A = host pack (plan.py _kde_pack_bf16)
+// [block][quarter][16][8]: lane l loads point l & 15's slots 8 (l >> 4) .. +7 (16 B, 1 KiB per
+// wave and block); B = kde_bf16_ops, 4 VGPRs per tile; D: the 16x16x4 form's layout, so
+// kde_reduce_tiles finishes the per-particle sums.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+struct KdeBOps {
+  bf16x8 b[4];      // tile t: particle 16 t + (lane & 15), slots 8 (lane >> 4) .. +7
+};
+
+__device__ __forceinline__ void bf16_split3(float v, __bf16 (&p)[3]) {
+  p[0] = (__bf16)v;
+  const float r1 = v - (float)p[0];
+  p[1] = (__bf16)r1;
+  p[2] = (__bf16)(r1 - (float)p[1]);
 }
 
-// per-lane partial sums of exp2(arg) over 16-point blocks [b0, b1) of pack kq, b1 - b0 a
-// multiple of 4 (padding blocks have weight 0); sums in packed pairs (v_pk_add_f32).  nx holds
-// blocks b0 .. b0+3 on entry (kde_prefetch4) and b1 .. b1+3 on return: each trip loads the
-// next trip's four operands before its 16 MFMAs and 64 exps.
-template <bool ZC>
-__device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int b0, int b1, int blast,
-                                              const KdeOps& o, int lane, float (&s)[4], float (&nx)[4]) {
-  f32x4 cin[4];
+// slot k (0..31) of the B operand: feature splits sp (_BF16_B pattern), -1 x 3, split of -|x'|^2
+__device__ __forceinline__ __bf16 kde_bslot(int k, int nf, const __bf16 (&sp)[3][3], const __bf16 (&sx)[3]) {
+  constexpr int pat[6] = {0, 0, 1, 0, 2, 1};
+  if (k < 18) return (k / 6) < nf ? sp[k / 6][pat[k % 6]] : (__bf16)0.f;
+  if (k < 21) return (__bf16)-1.f;
+  if (k < 24) return sx[k - 21];
+  return (__bf16)0.f;
+}
+
+// -|x'|^2 exactly as kde_own accumulates it
+__device__ __forceinline__ void kde_bf16_ops(const Lane& L, const int (&slots)[4], const float (&scl)[4], int nf,
+                                             KdeBOps& o) {
+  const int g = L.lane >> 4, n = L.lane & 15;
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
-    cin[t] = ZC ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4{o.negsq[t], o.negsq[t], o.negsq[t], o.negsq[t]};
+  for (int t = 0; t < 4; ++t) {
+    float sq = 0.f;
+    __bf16 sp[3][3], sx[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const float v = f < nf ? scl[f] * L.vals[slots[f] * WAVE + 16 * t + n] : 0.f;
+      if (f < nf) sq = fmaf(v, v, sq);
+      bf16_split3(2.f * v, sp[f]);
+    }
+    bf16_split3(-sq, sx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const __bf16 v0 = kde_bslot(j, nf, sp, sx), v1 = kde_bslot(8 + j, nf, sp, sx);
+      const __bf16 v2 = kde_bslot(16 + j, nf, sp, sx), v3 = kde_bslot(24 + j, nf, sp, sx);
+      o.b[t][j] = g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+    }
+  }
+}
+
+// per-lane tile partial sums of exp2(arg) over 16-point blocks [b0, b1) of the bf16x3 pack
+// (pa = pack + lane), b1 - b0 a multiple of 4; nx holds blocks b0 .. b0+3 on entry and
+// b1 .. b1+3 on return (kde_bf16_prefetch4): each trip loads the next trip's four operands
+// before its 16 MFMAs and 64 exps.
+__device__ __forceinline__ void kde_bf16_prefetch4(const bf16x8* __restrict__ pa, int b0, int blast, bf16x8 (&nx)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) nx[u] = pa[KDE_BLK(min(b0 + u, blast)) * 64];
+}
+
+__device__ __forceinline__ void kde_bf16_sums(const bf16x8* __restrict__ pa, int b0, int b1, int blast,
+                                              const KdeBOps& o, float (&s)[4], bf16x8 (&nx)[4]) {
   f32x2 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x2{0.f, 0.f};
   for (int b = b0; b < b1; b += 4) {
-    const float a[4] = {nx[0], nx[1], nx[2], nx[3]};
+    const bf16x8 a[4] = {nx[0], nx[1], nx[2], nx[3]};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) nx[u] = kq[KDE_BLK(min(b + 4 + u, blast)) * 64 + lane];   // next trip's operands
+    for (int u = 0; u < 4; ++u) nx[u] = pa[KDE_BLK(min(b + 4 + u, blast)) * 64];   // next trip's operands
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       f32x4 d[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) d[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], o.b[t], cin[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t)
+        d[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], o.b[t], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const f32x2 e01 = f32x2{__builtin_amdgcn_exp2f(d[t][0]), __builtin_amdgcn_exp2f(d[t][1])};
@@ -1353,61 +1376,6 @@ __device__ __forceinline__ void kde_mfma_sums(const float* __restrict__ kq, int 
   }
 #pragma unroll
   for (int t = 0; t < 4; ++t) s[t] += acc[t].x + acc[t].y;
-}
-
-__device__ __forceinline__ void kde_sums(const float* __restrict__ kq, int b0, int b1, int blast, const KdeOps& o,
-                                         int nf, int lane, float (&s)[4], float (&nx)[4]) {
-  if (nf <= 2) kde_mfma_sums<true>(kq, b0, b1, blast, o, lane, s, nx);
-  else kde_mfma_sums<false>(kq, b0, b1, blast, o, lane, s, nx);
-}
-
-// One-feature nodes: pass-1 sums on v_mfma_f32_32x32x2_f32 (1024 pairs per instruction, half
-// the matrix-pipe time of the 16x16x4 form): rows = 32 points (A = (y', |y'|^2), pack kq32
-// [block32][2][32]), columns = the 32 particles of tile t (B = (2x', -1)), C = -|x'|^2, i.e.
-// d = fmaf(|y'|^2, -1, fmaf(y', 2x', -|x'|^2)) (kde_arg_rec with nf < 0 replicates it).  Lane
-// (h, n) sums the exps of rows row(r, h) for particle 32 t + n; the two halves of both tiles
-// are added with one v_permlane32_swap per chunk.  pa = kq32 + lane; r = a ring of the next
-// three 32-point blocks' operands (blocks b0 .. b0+2 on entry, b1 .. b1+2 on return), so each
-// load is issued three blocks (~6 MFMAs and 48 exps of this wave) before its use.
-__device__ __forceinline__ void kde_mfma32_sums(const float* __restrict__ pa, int b0, int b1, int blast,
-                                                float bt0, float bt1, float ct0, float ct1, float (&s)[2],
-                                                float (&r)[3]) {
-  f32x16 c0, c1;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { c0[i] = ct0; c1[i] = ct1; }
-  f32x2 acc0 = f32x2{0.f, 0.f}, acc1 = f32x2{0.f, 0.f};
-  if (b1 <= b0) return;
-  auto take = [&](int i) {                     // block i's operand; block i + 3's load issued
-    const float a = r[0];
-    r[0] = r[1];
-    r[1] = r[2];
-    r[2] = pa[KDE_BLK(min(i + 3, blast)) * 64];
-    return a;
-  };
-  // software pipeline: the exps of one MFMA run while the next MFMA is in the matrix pipe
-  const float a0 = take(b0);
-  f32x16 q = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bt1, c1, 0, 0, 0);
-  f32x16 d = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, bt0, c0, 0, 0, 0);
-#pragma unroll
-  for (int i = 0; i < 16; i += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[i]), __builtin_amdgcn_exp2f(d[i + 1])};
-#pragma unroll 3
-  for (int i = b0 + 1; i < b1; ++i) {
-    const float a = take(i);
-    __builtin_amdgcn_sched_barrier(0);
-    d = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt0, c0, 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[k]), __builtin_amdgcn_exp2f(q[k + 1])};
-    __builtin_amdgcn_sched_barrier(0);
-    q = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bt1, c1, 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) acc0 += f32x2{__builtin_amdgcn_exp2f(d[k]), __builtin_amdgcn_exp2f(d[k + 1])};
-  }
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) acc1 += f32x2{__builtin_amdgcn_exp2f(q[k]), __builtin_amdgcn_exp2f(q[k + 1])};
-  s[0] += acc0.x + acc0.y;
-  s[1] += acc1.x + acc1.y;
 }
 
 // Inverse-CDF scan of one chunk [j0, j1) (pass 2).  A lane whose threshold lies in the upper
@@ -1452,13 +1420,11 @@ __device__ __forceinline__ int kde_scan(const float4* __restrict__ rec, const fl
 // VALU relative to their largest weight.
 __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
                                               float ucat, float c_p) {
-  const float* __restrict__ kq = L.P + st.reserved[1];
   const int M = st.k, nf = st.aux0, lane = L.lane;
   const int cb = kde_cb(M);
   int slots[4] = {0, 0, 0, 0};
   float scl[4] = {c_p, c_p, c_p, c_p};
   for (int f = 0; f < nf; ++f) slots[f] = L.ic[st.in_off + f];
-  const bool k32 = nf == 1 && st.reserved[7] >= 0;   // one-feature node with the 32x32x2 pack
   double tot = 0.0;
   float xv[4] = {0.f, 0.f, 0.f, 0.f};
   const float negsq = kde_own(L, slots, scl, nf, xv);
@@ -1488,37 +1454,22 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
     for (int ch = 0; ch < KDE_CHUNKS; ++ch) { L.scr[ch * WAVE + lane] = 1.f; tot += 1.0; }
   } else
 #endif
-  if (k32) {
-    const float* __restrict__ pa = L.P + st.reserved[7] + lane;
-    const int h = lane >> 5, n = lane & 31;
-    const float v0 = c_p * L.vals[slots[0] * WAVE + n], v1 = c_p * L.vals[slots[0] * WAVE + 32 + n];
-    const float bt0 = h ? -1.f : 2.f * v0, bt1 = h ? -1.f : 2.f * v1;
-    const float ct0 = -fmaf(v0, v0, 0.f), ct1 = -fmaf(v1, v1, 0.f);
-    const int cbh = cb >> 1, blast = KDE_CHUNKS * cbh - 1;
-    float ring[3] = {pa[0], pa[min(1, blast) * 64], pa[min(2, blast) * 64]};
-    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-      float s2[2] = {0.f, 0.f};
-      kde_mfma32_sums(pa, ch * cbh, ch * cbh + cbh, blast, bt0, bt1, ct0, ct1, s2, ring);
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2[0]), __float_as_uint(s2[1]), false, false);
-      const float cs = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-      L.scr[ch * WAVE + lane] = cs;
-      tot += (double)cs;
-    }
-  } else {
-    KdeOps o;
-    kde_operands(L, slots, scl, nf, o);
+  {
+    const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
+    KdeBOps o;
+    kde_bf16_ops(L, slots, scl, nf, o);
     const int blast = KDE_CHUNKS * cb - 1;
-    float nx[4];
-    kde_prefetch4(kq, 0, blast, lane, nx);
+    bf16x8 nx[4];
+    kde_bf16_prefetch4(pa, 0, blast, nx);
     for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
       float s[4] = {0.f, 0.f, 0.f, 0.f};
-      kde_sums(kq, ch * cb, ch * cb + cb, blast, o, nf, lane, s, nx);
+      kde_bf16_sums(pa, ch * cb, ch * cb + cb, blast, o, s, nx);
       const float cs = kde_reduce_tiles(s, lane);
       L.scr[ch * WAVE + lane] = cs;
       tot += (double)cs;
     }
   }
-  const int nfr = k32 ? -1 : nf;                      // replica form of the pass-1 elements
+  const int nfr = nf;                                 // replica form of the pass-1 elements
   const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
   // per-point records (4 weight-0 rows before the first point), then the reversed copy
   const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
@@ -1560,10 +1511,7 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   const float4* __restrict__ rev = rec + (((M + 15) >> 4) * 16 + KDE_REC_TAIL);
   int idx;
   // the replica chain per feature count, compile-time (kde_arg_rec)
-  if (nfr == -1)
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
-                   [&](const float4 r) { return fmaf(r.y, -1.f, fmaf(r.x, xb0, negsq)); });
-  else if (nfr == 1)
+  if (nfr == 1)
     idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
                    [&](const float4 r) { return fmaf(1.f, negsq, fmaf(r.y, -1.f, fmaf(r.x, xb0, 0.f))); });
   else if (nfr == 2)
@@ -1593,20 +1541,22 @@ __device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L,
   for (int d = 0; d < D; ++d) { slots[dp + d] = st.out_col + d; scl[dp + d] = c_y; }
   float sy4[4] = {0.f, 0.f, 0.f, 0.f}, sp4[4] = {0.f, 0.f, 0.f, 0.f};
   {
-    KdeOps oy;
-    kde_operands(L, slots, scl, dp + D, oy);
-    float nx[4];
-    kde_prefetch4(L.P + st.reserved[2], 0, nb - 1, lane, nx);
-    kde_sums(L.P + st.reserved[2], 0, nb, nb - 1, oy, dp + D, lane, sy4, nx);
+    const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[2]) + lane;
+    KdeBOps oy;
+    kde_bf16_ops(L, slots, scl, dp + D, oy);
+    bf16x8 nx[4];
+    kde_bf16_prefetch4(pa, 0, nb - 1, nx);
+    kde_bf16_sums(pa, 0, nb, nb - 1, oy, sy4, nx);
   }
   const float sy = kde_reduce_tiles(sy4, lane);
   float sp = 1.f;
   if (!root) {
-    KdeOps op;
-    kde_operands(L, slots, scl, dp, op);
-    float nx[4];
-    kde_prefetch4(L.P + st.reserved[1], 0, nb - 1, lane, nx);
-    kde_sums(L.P + st.reserved[1], 0, nb, nb - 1, op, dp, lane, sp4, nx);
+    const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
+    KdeBOps op;
+    kde_bf16_ops(L, slots, scl, dp, op);
+    bf16x8 nx[4];
+    kde_bf16_prefetch4(pa, 0, nb - 1, nx);
+    kde_bf16_sums(pa, 0, nb, nb - 1, op, sp4, nx);
     sp = kde_reduce_tiles(sp4, lane);
   }
   wave_sync();

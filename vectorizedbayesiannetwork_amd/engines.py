@@ -42,7 +42,7 @@ import torch
 
 from . import ops
 from .model import BNModel, model_from_vbn
-from .plan import (MODE_MCM, MODE_SAMPLE, MODE_WEIGHTED, GibbsPlan, PackedModel, QueryPlan, barren_pruned,
+from .plan import (KIND_ID, MODE_MCM, MODE_SAMPLE, MODE_WEIGHTED, GibbsPlan, PackedModel, QueryPlan, barren_pruned,
                    liveness_order, precompute_plans,
                    build_gibbs_plan, build_plan)
 from .registry import register_inference, register_sampling
@@ -244,6 +244,17 @@ def noise_tensor(pk: PackedModel, plan: QueryPlan, noise: Dict[str, Tuple], b: i
     return out.to(pk.device)
 
 
+# KDE walks launched in generations of about GEN_WAVES waves (0: one launch; env VBN_GEN_WAVES)
+GEN_WAVES = int(os.environ.get("VBN_GEN_WAVES", "0"))
+
+
+def _generations(plan: QueryPlan, b: int, n: int) -> int:
+    if GEN_WAVES <= 0 or not (plan.kind_mask & (1 << KIND_ID["kde"])) or n % 64:
+        return 1
+    waves = b * n // 64
+    return max(1, min(b, round(waves / GEN_WAVES)))
+
+
 def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: int, *,
              seed: int, offset: int = 0, q_base: int = 0, noise=None,
              fixed_per_particle: bool = False, state: Optional[torch.Tensor] = None, state_flags: int = 0,
@@ -304,7 +315,25 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
             plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
             len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
             plan.mode != MODE_SAMPLE, plan.kind_mask)
-    if state is None:
+    gens = _generations(plan, b, n) if (state is None and noise is None and not fixed_per_particle) else 1
+    if gens > 1:
+        # KDE walks in launches of about one resident wave per slot (GEN_WAVES): all waves of a
+        # launch start at the first node together and stay near each other in the node
+        # sequence, so the point packs they stream stay in L2 (scripts/gen_ab.py); per-query
+        # draws are keyed by q_base + query, so the outputs are the single launch's
+        step = -(-b // gens)
+        lps, xss = [], []
+        for b0 in range(0, b, step):
+            b1 = min(b, b0 + step)
+            fx = fixed[b0:b1] if fixed.shape[0] == b else fixed
+            a = args[:3] + (fx,) + args[4:6] + (b1 - b0,) + args[7:17] + (q_base + b0,) + args[18:]
+            l, x = ops.walk(*a, plan.wbuf, plan_jit, precomp,
+                            precomp_q[b0:b1] if precomp_q is not None else None)
+            lps.append(l.view(b1 - b0, n) if plan.mode != MODE_SAMPLE else l)
+            xss.append(x.view(b1 - b0, n, -1) if n_out_cols else x)
+        lp = torch.cat(lps) if plan.mode != MODE_SAMPLE else lps[0]
+        x = torch.cat(xss) if n_out_cols else xss[0]
+    elif state is None:
         lp, x = ops.walk(*args, plan.wbuf, plan_jit, precomp, precomp_q)
     else:
         lp, x = ops.walk_segment(*args, state, state_flags, step_begin, step_end, plan.wbuf)

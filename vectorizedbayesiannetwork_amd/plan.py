@@ -39,7 +39,7 @@ STEP_INTS = 32
 (S_KIND, S_ROLE, S_FLAGS, S_ACT, S_NIN, S_INOFF, S_OUTCOL, S_OUTDIM, S_FIXEDCOL, S_K, S_NOUT,
  S_NODEID, S_NOISE, S_AUX0, S_AUX1, S_AUX2, S_OFF_STD, S_OFF_W1, S_OFF_W2, S_OFF_B2, S_OFF_W3,
  S_OFF_B3, S_OFF_TAIL, S_OFF_PTS, S_OFF_W2H, S_OFF_KQ, S_OFF_KQY, S_OFF_KR, S_OFF_KV,
- S_WBLK_OFF, S_WBLK_LEN, S_OFF_KQ32) = range(32)
+ S_WBLK_OFF, S_WBLK_LEN, S_RES7) = range(32)
 WBLK_CHUNK = 256          # floats per LDS-DMA wave instruction (64 lanes x 16 B)
 KDE_CHUNKS = 16
 KDE_REC_TAIL = 8       # weight-0 record rows after the last point (csrc kde_scan prefetch)
@@ -123,20 +123,59 @@ def _kde_pack(feats: List[np.ndarray], records: bool = False) -> np.ndarray:
     return a.reshape(rows // 16, 16, 4).transpose(0, 2, 1)
 
 
-def _kde_pack32(y: np.ndarray) -> np.ndarray:
-    """One-feature point pack of the 32x32x2 pass (csrc kde_mfma32_sums): per 32-point block
-    [y'_0..y'_31 | |y'|^2_0..|y'|^2_31]; the same points, |y'|^2 and padding (1e30) as
-    _kde_pack, so the chunk boundaries (multiples of 64 points) coincide."""
+def _bf16_split3(v: np.ndarray):
+    """f32 -> three bf16 (round to nearest even) whose sum is v exactly: hi = bf16(v),
+    mid = bf16(v - hi), lo = v - hi - mid (8 significant bits left, exact); uint16 bits."""
+    def rne(x):
+        b = x.astype(np.float32).view(np.uint32).astype(np.uint64)
+        return ((b + 0x7FFF + ((b >> 16) & 1)) >> 16).astype(np.uint16)
+
+    def val(h):
+        return (h.astype(np.uint32) << 16).view(np.float32)
+    v = v.astype(np.float32)
+    hi = rne(v)
+    r1 = (v - val(hi)).astype(np.float32)
+    mid = rne(r1)
+    r2 = (r1 - val(mid)).astype(np.float32)
+    lo = rne(r2)
+    return hi, mid, lo
+
+
+# bf16x3 slot pattern of one feature: A (point y') side and B (particle u = 2x') side, so the
+# six products are u_h y_h, u_h y_m, u_m y_h, u_h y_l, u_l y_h, u_m y_m (csrc kde_bf16_sums)
+_BF16_A = (0, 1, 0, 2, 0, 1)
+_BF16_B = (0, 0, 1, 0, 2, 1)
+KDE_BF16_K = 32                       # slots per point (v_mfma_f32_16x16x32_bf16)
+
+
+def _kde_pack_bf16(y: np.ndarray) -> np.ndarray:
+    """Point pack of the bf16x3 pass (csrc kde_bf16_sums): A operand of
+    v_mfma_f32_16x16x32_bf16, rows = 16 points per block, K = 32 slots per point: feature f at
+    slots 6f .. 6f+5 (_BF16_A of its hi / mid / lo split; zero for f >= nf), |y'|^2's hi / mid /
+    lo at 18-20 (B side -1), 1.0 at 21-23 (B side: the split of -|x'|^2), 24-31 zero.  Layout
+    [block][quarter][16 points][8 slots] bf16 (lane l loads point l & 15's slots 8 (l >> 4) ..
+    +7 as one 16-byte load); the same points, |y'|^2, padding (|y'|^2 = 1e30) and blocks as
+    _kde_pack (KDE_CHUNKS * cb blocks of 16), so chunk boundaries coincide."""
     y = y.reshape(y.shape[0], -1).astype(np.float32)
     m, nf = y.shape
-    if nf != 1:
-        raise ValueError("the 32x32x2 pack is for one-feature nodes")
-    rows = KDE_CHUNKS * _kde_cb(m) * 16
-    a = np.zeros((rows, 2), np.float32)
-    a[:, 1] = 1e30
-    a[:m, 0] = y[:, 0]
-    a[:m, 1] = (y.astype(np.float64) ** 2).sum(axis=1).astype(np.float32)
-    return a.reshape(rows // 32, 32, 2).transpose(0, 2, 1)
+    if not 1 <= nf <= 3:
+        raise ValueError("the bf16x3 KDE pack is for 1-3 features")
+    nblk = KDE_CHUNKS * _kde_cb(m)
+    rows = nblk * 16
+    feats = np.zeros((rows, nf), np.float32)
+    feats[:m] = y
+    sq = np.full(rows, 1e30, np.float32)
+    sq[:m] = (y.astype(np.float64) ** 2).sum(axis=1).astype(np.float32)
+    slots = np.zeros((rows, KDE_BF16_K), np.uint16)
+    for f in range(nf):
+        sp = _bf16_split3(feats[:, f])
+        for j in range(6):
+            slots[:, 6 * f + j] = sp[_BF16_A[j]]
+    for j, h in enumerate(_bf16_split3(sq)):
+        slots[:, 18 + j] = h
+    slots[:, 21:24] = 0x3F80                                  # bf16 1.0
+    a = slots.reshape(nblk, 16, 4, 8).transpose(0, 2, 1, 3)   # [blk][quarter][16][8]
+    return np.ascontiguousarray(a).reshape(-1).view(np.float32)
 
 
 def _kde_pack_valu(y: np.ndarray) -> np.ndarray:
@@ -343,15 +382,15 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
         c_y = np.float32(_KDE_C / s_y)
         offs["tail"] = blob.add(np.array([1.0 / np.float32(s_p), 1.0 / np.float32(s_y),
                                           noise_scale, cy, math.log(float(m)), c_p, c_y, 0], np.float32))
-        # MFMA packs (csrc/vbn_walk_impl.h, kde_mfma_sums): [block][k][16] point features
+        # MFMA packs (csrc/vbn_walk_impl.h, kde_bf16_sums): bf16x3 point slots, [block][quarter][16][8]
         if 1 <= dp <= 3:
-            offs["kq"] = blob.add(_kde_pack([_np(pts_p) * c_p]))
+            offs["kq"] = blob.add(_kde_pack_bf16(_np(pts_p) * c_p))
             offs["kr"] = blob.add(_kde_pack([_np(pts_p) * c_p], records=True))
             offs["kv"] = blob.add(_kde_pack_valu(_np(pts_p) * c_p))
-            if dp == 1:
-                offs["kq32"] = blob.add(_kde_pack32(_np(pts_p) * c_p))
         if dp + D <= 3:
-            offs["kqy"] = blob.add(_kde_pack(([_np(pts_p) * c_p] if dp else []) + [_np(pts_y) * c_y]))
+            feats = np.concatenate(([_np(pts_p).reshape(m, -1) * c_p] if dp else [])
+                                   + [_np(pts_y).reshape(m, -1) * c_y], axis=1)
+            offs["kqy"] = blob.add(_kde_pack_bf16(feats))
         stride = dp + D
         stride += (-stride) % 2 if stride > 1 else 0
         recs = np.zeros((m, stride), np.float32)
@@ -663,7 +702,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
             row[S_FLAGS] = fl
         row[S_OFF_KR] = npk.offs.get("kr", -1)
         row[S_OFF_KV] = npk.offs.get("kv", -1)
-        row[S_OFF_KQ32] = npk.offs.get("kq32", -1)
+        row[S_RES7] = -1
         if "wblk" in npk.offs and (n in latent_s or n in logp_s or n in params_s):
             row[S_WBLK_OFF] = npk.offs["wblk"]
             row[S_WBLK_LEN] = npk.offs["wblk_len"]
