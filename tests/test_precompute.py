@@ -48,7 +48,7 @@ def _want(model, vals, plan, shared):
     return ws, wq
 
 
-def _check_cols(model, pk, rows, nodes, stride):
+def _check_cols(model, pk, rows, nodes, stride, width=None):
     cols = []
     for i, n in enumerate(model.topo):
         if n not in nodes:
@@ -61,7 +61,7 @@ def _check_cols(model, pk, rows, nodes, stride):
         assert r[P.S_WBLK_LEN] == 0                          # no MLP runs: nothing to stage
     cols.sort()
     assert cols[0][0] == 0 and all(a + w == c for (a, w), (c, _) in zip(cols, cols[1:]))
-    assert cols[-1][0] + cols[-1][1] == stride
+    assert cols[-1][0] + cols[-1][1] == (stride if width is None else width)
 
 
 @pytest.mark.parametrize("cfg_name,engine", [("cfg2", "mcm"), ("cfg4", "mcm"), ("cfg5", "mcm"), ("anchor64", "mcm"),
@@ -105,9 +105,10 @@ def test_precompute_marks_nodes(cfg_name, engine):
         assert pre is None and not hasattr(pc.steps, "_vbn_precomp_stride")
     # the per-query pre-pass: the main walk's fixed steps (same fixed-buffer columns), then the
     # candidates writing their quantities
+    # the walk reads row 64 b of the pre-pass's [B * 64, w] out_x in place: stride 64 w
     stride_q = pc.steps._vbn_precomp_q_stride
-    assert stride_q == pre_q.out_cols.numel()
-    _check_cols(model, pk, rows, got_q, stride_q)
+    assert stride_q == 64 * pre_q.out_cols.numel()
+    _check_cols(model, pk, rows, got_q, stride_q, width=pre_q.out_cols.numel())
     assert pre_q.fixed_nodes == plan.fixed_nodes and pre_q.fixed_ld == plan.fixed_ld
     qrow = pre_q.steps._vbn_host[0]
     qorder = [n for n in model.topo if n in vals or n in got_q]

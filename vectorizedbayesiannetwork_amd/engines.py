@@ -255,6 +255,27 @@ def _generations(plan: QueryPlan, b: int, n: int) -> int:
     return max(1, min(b, round(waves / GEN_WAVES)))
 
 
+def _query_rows(pq: torch.Tensor, b: int, steps: torch.Tensor) -> torch.Tensor:
+    """The per-query pre-pass's out_x [b * 64, w] as the walk's precomp_q: read in place as
+    [b, 64 w] when the step table's stride is 64 w (plan.precompute_plans), else row 64 b
+    gathered into [b, w]."""
+    w = pq.shape[-1]
+    if getattr(steps, "_vbn_precomp_q_stride", None) == 64 * w:
+        return pq.view(b, 64 * w)
+    return pq.view(b, 64, w)[:, 0].contiguous()
+
+
+_SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(device: torch.device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _SIDE_STREAMS.get(idx)
+    if s is None:
+        s = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=torch.device("cuda", idx))
+    return s
+
+
 def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: int, *,
              seed: int, offset: int = 0, q_base: int = 0, noise=None,
              fixed_per_particle: bool = False, state: Optional[torch.Tensor] = None, state_flags: int = 0,
@@ -298,12 +319,22 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
         # seed / offset: the pre-pass draws the main walk's root values), the per-query ones of
         # nodes with evidence parents, once per query (one wave of identical lanes), then the
         # main walk
+        # with both, the per-sample one (a few waves walking the root nodes, latency-bound) runs
+        # on a side stream next to the per-query one
+        side = _side_stream(pk.device) if (plan.pre is not None and plan.pre_q is not None) else None
+        if side is not None:
+            main = torch.cuda.current_stream(pk.device)
+            side.wait_stream(main)
         if plan.pre is not None:
-            _, precomp = run_walk(pk, plan.pre, fixed, 1, n, seed=seed, offset=offset, plan_jit=0)
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                _, precomp = run_walk(pk, plan.pre, fixed, 1, n, seed=seed, offset=offset, plan_jit=0)
             precomp = precomp.view(n, -1)
         if plan.pre_q is not None:
             _, pq = run_walk(pk, plan.pre_q, fixed, b, 64, seed=seed, offset=offset, q_base=q_base, plan_jit=0)
-            precomp_q = pq.view(b, 64, -1)[:, 0].contiguous()
+            precomp_q = _query_rows(pq, b, plan.pc.steps)
+        if side is not None:
+            main.wait_stream(side)
+            precomp.record_stream(main)
         walk_plan = plan.pc
         pre_ran = True
     # (the plan as given: a re-run of this launch repeats the pre-passes)

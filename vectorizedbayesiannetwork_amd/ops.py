@@ -609,7 +609,9 @@ def _query_walk(plan, params, fixed, n_samples, seed, offset, q_base, noise, pla
         precomp = x.view(n_samples, -1)
     if secs[3] is not None:
         _, x = _section_walk(secs[3], params, fixed, b, 64, seed, offset, q_base, None, 0)
-        precomp_q = x.view(b, 64, -1)[:, 0].contiguous()
+        w = x.shape[-1]
+        precomp_q = (x.view(b, 64 * w) if getattr(secs[1][0], "_vbn_precomp_q_stride", None) == 64 * w
+                     else x.view(b, 64, w)[:, 0].contiguous())
     return _section_walk(secs[1], params, fixed, b, n_samples, seed, offset, q_base, None, plan_jit,
                          precomp, precomp_q), secs[1]
 

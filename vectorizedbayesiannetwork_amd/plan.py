@@ -1008,6 +1008,10 @@ def precompute_plans(packed: PackedModel, plan: QueryPlan, *, skip: Sequence[str
                                     fixed_ld=plan.fixed_ld)
     for cands, extra in ((cand_s, 0), (cand_q, F_PRECOMP_Q)):
         stride = sum(precompute_width(packed, n) for n in cands)
+        if extra and 64 * stride < (1 << 15):
+            # the per-query pre-pass writes 64 identical rows per query: the walk reads row
+            # 64 b of its out_x in place (stride 64 x width, engines.run_walk), no gather copy
+            stride *= 64
         assert stride < (1 << 15)
         col = 0
         for n in cands:
