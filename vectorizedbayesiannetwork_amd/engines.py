@@ -265,6 +265,8 @@ def _query_rows(pq: torch.Tensor, b: int, steps: torch.Tensor) -> torch.Tensor:
     return pq.view(b, 64, w)[:, 0].contiguous()
 
 
+# the per-sample pre-pass on a side stream next to the per-query one (env VBN_PRE_STREAM=0: off)
+PRE_SIDE_STREAM = os.environ.get("VBN_PRE_STREAM", "1") != "0"
 _SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
 
 
@@ -321,7 +323,8 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
         # main walk
         # with both, the per-sample one (a few waves walking the root nodes, latency-bound) runs
         # on a side stream next to the per-query one
-        side = _side_stream(pk.device) if (plan.pre is not None and plan.pre_q is not None) else None
+        side = (_side_stream(pk.device) if (PRE_SIDE_STREAM and plan.pre is not None and plan.pre_q is not None)
+                else None)
         if side is not None:
             main = torch.cuda.current_stream(pk.device)
             side.wait_stream(main)
