@@ -389,6 +389,44 @@ __device__ __forceinline__ f32x16 layer2_split(const uint4 (&w2h)[4], const f32x
   return b;
 }
 
+// Layer 2 of one group from the raw layer-1 pre-activations z with the ReLU folded into the
+// f16 split (the caller guarantees z < 2048): hi = f16 of z rounded toward zero, so the
+// residual z - hi lies in [0, 1) for z >= 0 and in (-1, 0] for z < 0; one v_fma_mix_f32 with
+// the clamp bit ([0, 1]) then gives relu(z) - relu(hi) exactly, and one v_pk_max_f16 per pair
+// gives relu(hi): hi + lo = relu(z) to f16 x f16 precision, 5 VALU per pair of activations
+// instead of 6 (two ReLU maxes, two conversions, two residuals).
+__device__ __forceinline__ f32x16 layer2_split_relu(const uint4 (&w2h)[4], const f32x16& binit,
+                                                    const float (&z)[16]) {
+  f16x8 bh[2], bl[2];
+  const f16x2 zero2 = {(_Float16)0.f, (_Float16)0.f};
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const float z0 = z[8 * s2 + j], z1 = z[8 * s2 + j + 1];
+      const f16x2 pr = __builtin_bit_cast(f16x2, __builtin_amdgcn_cvt_pkrtz(z0, z1));
+      const float r0 = __builtin_amdgcn_fmed3f(sub_f16_lo(z0, pr), 0.f, 1.f);
+      const float r1 = __builtin_amdgcn_fmed3f(sub_f16_hi(z1, pr), 0.f, 1.f);
+      const f16x2 pl = __builtin_convertvector((f32x2){r0, r1}, f16x2);
+      const f16x2 ph = __builtin_elementwise_max(pr, zero2);
+      bh[s2][j] = ph[0];
+      bh[s2][j + 1] = ph[1];
+      bl[s2][j] = pl[0];
+      bl[s2][j + 1] = pl[1];
+    }
+  }
+  f32x16 b = binit;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const f16x8 ah = __builtin_bit_cast(f16x8, w2h[s2]);
+    const f16x8 al = __builtin_bit_cast(f16x8, w2h[2 + s2]);
+    b = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s2], b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s2], b, 0, 0, 0);
+    b = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s2], b, 0, 0, 0);
+  }
+  return b;
+}
+
 // Layer 2 of one group from the activations y, exact f32 chain (K = 32 as 16
 // v_mfma_f32_32x32x2_f32 steps)
 __device__ __forceinline__ f32x16 layer2_exact(const vbn_step& st, const Lane& L, int g, const float (&y)[16]) {
@@ -477,7 +515,7 @@ __device__ __forceinline__ void mlp_head(const vbn_step& st, const Lane& L, cons
 // compare per MFMA operand instead of one max per activation; CHK = 1 -- some activation
 // leaves the split range |y| <= 32768 (NaN with the sign bit clear counts as out of range).
 #define VBN_ZLIM(st) __int_as_float((st).reserved[1])
-template <int ACT, bool STD, int NIN, int CHK = 0, typename F>
+template <int ACT, bool STD, int NIN, int CHK = 0, bool RAW = false, typename F>
 __device__ __forceinline__ bool mlp_l1_act(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
                                            const float* __restrict__ W, int g, float (&y)[16], F&& pre) {
   const int lane = L.lane;
@@ -507,10 +545,11 @@ __device__ __forceinline__ bool mlp_l1_act(const vbn_walk_args& A, const vbn_ste
   int big = 0;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    y[r] = act_fn<ACT>(a[r]);
+    y[r] = RAW ? a[r] : act_fn<ACT>(a[r]);                // RAW: relu folded into the split
     if (CHK == 1) big = max(big, __float_as_int(y[r]));   // activations are >= -1: the positive side
   }
-  return CHK == 1 ? __any(big > 0x47000000) : __any(out);
+  // split range: relu nodes (layer2_split_relu) z < 2048, others |act(z)| <= 32768
+  return CHK == 1 ? __any(big > (ACT == VBN_ACT_RELU ? 0x44ffffff : 0x47000000)) : __any(out);
 }
 
 // Head outputs with a compile-time count (NOUT > 0): straight-line code, so the scheduler can
@@ -598,16 +637,21 @@ __device__ __forceinline__ void mlp_forward(const vbn_walk_args& A, const vbn_st
   f32x16 h0, h1;
   bool beyond;                                    // some layer-1 operand beyond the node's bound
   {
+#ifdef VBN_ABL_NOFUSE      // A/B only: relu then the plain split (same outputs to f32 rounding)
+    constexpr bool FUSE = false;
+#else
+    constexpr bool FUSE = ACT == VBN_ACT_RELU;    // relu folded into the f16 split
+#endif
     float y[16];
-    beyond = mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 0, y, pre);
+    beyond = mlp_l1_act<ACT, STD, NIN, 0, FUSE>(A, st, L, W, 0, y, pre);
     const uint4 wq[4] = {w2h[lane], w2h[WAVE + lane], w2h[2 * WAVE + lane], w2h[3 * WAVE + lane]};
-    h0 = layer2_split(wq, load_acc16(b2), y);
+    h0 = FUSE ? layer2_split_relu(wq, load_acc16(b2), y) : layer2_split(wq, load_acc16(b2), y);
     if constexpr (MIR) {
       h1 = h0;                                    // group 1 = group 0's particles
     } else {
       float y1[16];
-      beyond |= mlp_l1_act<ACT, STD, NIN>(A, st, L, W, 1, y1, [] {});
-      h1 = layer2_split(wq, load_acc16(b2 + 32), y1);
+      beyond |= mlp_l1_act<ACT, STD, NIN, 0, FUSE>(A, st, L, W, 1, y1, [] {});
+      h1 = FUSE ? layer2_split_relu(wq, load_acc16(b2 + 32), y1) : layer2_split(wq, load_acc16(b2 + 32), y1);
     }
   }
   if constexpr (NOUT > 0) {

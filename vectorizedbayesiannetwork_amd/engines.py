@@ -265,8 +265,9 @@ def _query_rows(pq: torch.Tensor, b: int, steps: torch.Tensor) -> torch.Tensor:
     return pq.view(b, 64, w)[:, 0].contiguous()
 
 
-# the per-sample pre-pass on a side stream next to the per-query one (env VBN_PRE_STREAM=0: off)
-PRE_SIDE_STREAM = os.environ.get("VBN_PRE_STREAM", "1") != "0"
+# the per-sample pre-pass on a side stream next to the per-query one (env VBN_PRE_STREAM=1: on).
+# Off: measured 2-3 % slower walks on cfg2 / anchor64 (profiles/r04_bench/r04j_ab_*)
+PRE_SIDE_STREAM = os.environ.get("VBN_PRE_STREAM", "0") == "1"
 _SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
 
 

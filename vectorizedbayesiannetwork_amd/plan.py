@@ -254,10 +254,13 @@ def _pack_mlp(blob: _Blob, rec: CPDRecord, standardize: bool) -> Dict[str, int]:
     offs["f32l2"] = int(np.abs(w2).max() > 32768.0)
     # layer-1 operand bound (csrc mlp_l1_act): with every operand |x| <= zlim, each layer-1
     # pre-activation |z| <= max|b1| + zlim max_r sum_k |W1[r, k]| and |act(z)| <= max(|z|, 1)
-    # stay inside the f16 split range, so the walk compares the operands (one per MFMA) instead
+    # stay inside the split range, so the walk compares the operands (one per MFMA) instead
     # of every activation; 0.1 % margin for the f32 accumulation.  -1: no bound (always check)
+    # relu nodes split the raw pre-activation with the ReLU folded in (csrc
+    # layer2_split_relu), which needs z < 2048: the bound is taken against that
     rs = float(np.abs(w1.astype(np.float64)).sum(axis=1).max()) if w1.size else 0.0
-    room = 32768.0 * (1.0 - 1e-3) - float(np.abs(b1.astype(np.float64)).max())
+    lim = 2048.0 if str(rec.hp("activation") or "relu") == "relu" else 32768.0
+    room = lim * (1.0 - 1e-3) - float(np.abs(b1.astype(np.float64)).max())
     if room <= 1.0:
         offs["zlim"] = -1.0
     else:
