@@ -508,7 +508,7 @@ def barren_pruned(model: BNModel, keep: Sequence[str]) -> set:
 
 
 def liveness_order(model: BNModel, *, fixed: Sequence[str], logp: Sequence[str], out_nodes: Sequence[str],
-                   params: Sequence[str] = (), skip: Sequence[str] = ()) -> List[str]:
+                   params: Sequence[str] = (), skip: Sequence[str] = (), seed: Optional[int] = None) -> List[str]:
     """A topological order of the non-skipped nodes that keeps few node values live at once
     (greedy list scheduling: among the ready nodes, the one whose step frees the most parent
     columns and holds the fewest new ones; ties in the model's order).  Node values live in LDS
@@ -517,6 +517,9 @@ def liveness_order(model: BNModel, *, fixed: Sequence[str], logp: Sequence[str],
     skip_s, fixed_s, logp_s, params_s = set(skip), set(fixed), set(logp), set(params)
     nodes = [n for n in model.topo if n not in skip_s]
     rank = {n: i for i, n in enumerate(nodes)}
+    # ties broken in the model's order, or (seed given) in a seeded random order: a restart of
+    # the greedy, deterministic per seed
+    tie = rank if seed is None else dict(zip(nodes, np.random.default_rng(seed).permutation(len(nodes)).tolist()))
     reads = {n: (n not in fixed_s) or (n in logp_s) or (n in params_s) for n in nodes}
     children = {n: [] for n in nodes}
     for n in nodes:
@@ -533,7 +536,7 @@ def liveness_order(model: BNModel, *, fixed: Sequence[str], logp: Sequence[str],
             freed = sum(1 for p in model.parents[n] if p in rank and reads[n] and readers_left[p] == 1
                         and p not in outs)
             holds = 0 if (readers_left[n] == 0 and n not in outs) else 1
-            return (holds - freed, rank[n])
+            return (holds - freed, tie[n])
         n = min(ready, key=cost)
         ready.remove(n)
         order.append(n)
