@@ -2,7 +2,7 @@
 
 The liveness order is a topological order that keeps fewer node values live, so a wave needs
 fewer LDS slots; engines use it only where the plan's LDS bounds the waves per CU (cfg5's
-128-node DAG: 32 -> 25 slots, 13 -> 15 waves per CU).  Draws are keyed by node, so the order
+128-node DAG: 32 -> 25 slots with the greedy, 24 after seeded restarts: 13 -> 16 waves per CU).  Draws are keyed by node, so the order
 changes only the slot assignment and which normals share a Box-Muller pair; the host replica of
 the draws (tests/philox_draws.py) pairs by the step table, so the oracle comparisons of the GPU
 tests hold for any order.
@@ -51,6 +51,8 @@ def test_engine_uses_liveness_order_only_when_lds_bound():
         p = E._plan(pk, ("mcm", cfg, "test"), **kw)
         assert (p.order != list(model.topo)) == reordered
         assert E._lds_bound(base) == reordered
+        if reordered:                    # the restarted greedy ends the bound: 16 waves per CU
+            assert p.n_slots == 24 and not E._lds_bound(p)
 
 
 def test_box_muller_pairs_follow_the_table():
