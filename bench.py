@@ -2,10 +2,11 @@
 """Throughput of ``VBN.infer_posterior`` on MI355X (BASELINE.json metric).
 
 A step = one ``infer_posterior`` call over one batch of synthetic queries:
-default workload cfg2 = 32-node random DAG, gaussian_nn CPDs (random-init weights of the
-reference architecture, data-derived standardisation), 4096 queries x 1024 samples per GPU,
-monte_carlo_marginalization.  Every N runs the same path: the global batch (4096 x N
-queries) goes through ``ShardedEngine(engine, gather=True, overlap=True)`` -- each rank walks
+default workload cfg4 = 64-node random DAG, kde CPDs with 10,000 stored points each (the
+reference-fitted model: KDE fitting keeps the training rows), 4096 queries x 1024 samples per
+GPU, monte_carlo_marginalization -- BASELINE.json's largest single-GPU config and the
+north-star's 64-node target; ``--config cfg2`` etc. select the other workloads.  Every N
+runs the same path: the global batch (4096 x N queries) goes through ``ShardedEngine(engine, gather=True, overlap=True)`` -- each rank walks
 its contiguous 4096-query shard (weak scaling; the global query index keys the RNG) and the
 pdf / samples are gathered on rank 0 with one RCCL gather over xGMI per step, issued
 asynchronously so it overlaps the next step's walk (N = 1: no collective).
@@ -47,17 +48,26 @@ HBM_PEAK_GBS = 8000.0
 # v_exp_f32: 8 issue cycles per wave64 instruction per SIMD (MI355X_MICROARCH.md constants)
 # -> 8 exp/clk/SIMD x 1024 SIMDs x 2.4 GHz
 EXP_PEAK_T = 8 * 1024 * 2.4e9 / 1e12
+MODELS_DIR = os.path.join(REPO, "tests", "golden", "models")
 
 
 def build_model(cfg_name: str):
-    """The synthetic model of ``cfg_name``: random DAG, SEM data, random-init
-    CPDs of the reference architectures; returns (cfg, model, target, evidence nodes)."""
+    """The synthetic model of ``cfg_name``: random DAG, SEM data and the CPDs
+    the reference fitted on it (``tests/golden/models``, make_golden_models.py: YAML
+    hyper-parameters, one epoch of batch 4096); configs without a fitted fixture get random-init
+    CPDs of the reference architectures (``cfg["model_origin"]`` says which).  Returns (cfg,
+    model, target, evidence nodes)."""
     cfg = dict(synthetic.CONFIGS[cfg_name])
     g = synthetic.random_dag(cfg["n_nodes"], seed=0)
-    data = synthetic.sem_data(g, cfg.get("rows", 2048), seed=0)
-    kinds = synthetic.round_robin_kinds(g, cfg["kinds"])
-    overrides = {"kde": {"max_points": cfg["kde_max_points"]}} if "kde_max_points" in cfg else None
-    model = random_init_model(g, kinds, data, seed=0, overrides=overrides)
+    model = synthetic.fitted_model(cfg_name, MODELS_DIR)
+    origin = "reference-fitted"
+    if model is None:
+        data = synthetic.sem_data(g, cfg.get("rows", 2048), seed=0)
+        kinds = synthetic.round_robin_kinds(g, cfg["kinds"])
+        overrides = {"kde": {"max_points": cfg["kde_max_points"]}} if "kde_max_points" in cfg else None
+        model = random_init_model(g, kinds, data, seed=0, overrides=overrides)
+        origin = "random-init"
+    cfg["model_origin"] = origin
     target, ev_nodes = synthetic.default_query_nodes(g, seed=1)
     return cfg, model, target, ev_nodes
 
@@ -234,7 +244,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--config", default="cfg4",
+                    help="workload (vectorizedbayesiannetwork_amd/synthetic.py CONFIGS); default cfg4, the "
+                         "largest single-GPU config of BASELINE.json (64-node KDE DAG, M = 10k, 4096 x 1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-queries", type=int, default=0)
     ap.add_argument("--cpu-reps", type=int, default=5)
@@ -485,7 +497,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (SURVEY §8d DAG/SEM/query generator; random-init CPD weights)",
+        "data": f"synthetic (SURVEY §8d DAG/SEM/query generator; {cfg['model_origin']} CPDs)",
         "config": {"workload": f"{args.config}: {cfg['name']}", "queries_per_gpu": B, "global_batch": B * world,
                    "n_samples": S, "n_nodes": cfg["n_nodes"], "engine": cfg["engine"],
                    "parallelism": par, "gather": gather and dist, "prune_barren": args.prune_barren,
@@ -503,15 +515,16 @@ def main():
         out["gather"] = gather_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # a bounded sample of ~10-30 s of CPU work (the oracle's q/s is linear in B): cfg2 /
-        # anchor64 1024 queries, cfg3 (IS, ~100 q/s) 256, cfg5 (~0.7 q/s) 8, cfg4 (~0.2 q/s) 2
+        # anchor64 1024 queries, cfg3 (IS, ~100 q/s) 256, cfg5 (~0.7 q/s) 4, cfg4 (~0.2 q/s) 1;
+        # KDE configs time 3 repetitions after the warm-up (~5 s each), the others 5
         kde = "kde" in cfg["kinds"]
         if args.cpu_queries:
             nq = args.cpu_queries
         elif kde:
-            nq = 2 if cfg["kinds"] == ("kde",) else 8
+            nq = 1 if cfg["kinds"] == ("kde",) else 4
         else:
             nq = 1024 if cfg["engine"] == "monte_carlo_marginalization" else 256
-        reps_cpu = 2 if kde else args.cpu_reps
+        reps_cpu = min(3, args.cpu_reps) if kde else args.cpu_reps
         print(f"cpu baseline: {nq} queries in a child process ...", file=sys.stderr, flush=True)
         out["cpu_baseline"] = cpu_baseline(args.config, nq, reps_cpu)
     if rank == 0:

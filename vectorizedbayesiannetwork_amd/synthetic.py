@@ -56,6 +56,34 @@ def round_robin_kinds(g: nx.DiGraph, kinds: Sequence[str]) -> Dict[str, str]:
     return {node: kinds[i % len(kinds)] for i, node in enumerate(g.nodes)}
 
 
+def fitted_model(cfg_name: str, models_dir: str):
+    """The reference-fitted model of ``cfg_name`` (YAML hyper-parameters,
+    ``fit={"epochs": 1, "batch_size": 4096}``, fitted by the reference in the build container,
+    ``tests/golden/make_golden_models.py``), or None when ``models_dir`` has no fixture for it.
+
+    cfg4's fixture is a marker: its KDE nodes keep their 10,000 training rows unchanged
+    (M = ``max_points``), which the script checked bit for bit against the SEM data, so the
+    model is rebuilt from the data with the recorded init kwargs."""
+    import os
+
+    from .model import model_from_checkpoint, random_init_model
+    path = os.path.join(models_dir, f"{cfg_name}.pt")
+    if not os.path.exists(path):
+        return None
+    ck = torch.load(path, weights_only=True)
+    if ck.get("kde_points_are_sem_data"):
+        cfg = CONFIGS[cfg_name]
+        assert tuple(cfg["kinds"]) == ("kde",), f"{cfg_name}: the data marker is for KDE-only models"
+        g = random_dag(cfg["n_nodes"], seed=0)
+        data = sem_data(g, cfg.get("rows", 2048), seed=0)
+        model = random_init_model(g, round_robin_kinds(g, cfg["kinds"]), data, seed=0,
+                                  overrides={"kde": dict(ck["init_kwargs"])})
+        for rec in model.cpds.values():
+            assert rec.extra["targets"].shape[0] == int(ck["init_kwargs"]["max_points"])
+        return model
+    return model_from_checkpoint(ck)
+
+
 def default_query_nodes(g: nx.DiGraph, seed: int = 1) -> Tuple[str, List[str]]:
     topo = list(nx.topological_sort(g))
     target = topo[-1]
