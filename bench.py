@@ -398,13 +398,14 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pdf, samples = vbn.infer_posterior(query)
-        if hasattr(engine, "_last_fallback"):
-            fallbacks.append(bool(engine._last_fallback))
+        if hasattr(engine, "fallback_flag"):        # IS: the device flag, read after the timing
+            fallbacks.append(engine.fallback_flag())
     sharded.wait()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     gc.enable()
+    fallbacks = [bool(f.item()) for f in fallbacks if f is not None]
     if dist:
         t = torch.tensor([elapsed], device=device if args.dist_backend == "nccl" else "cpu", dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)

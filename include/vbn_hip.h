@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 10
+#define VBN_ABI_VERSION 11
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001
@@ -97,6 +97,16 @@ int vbn_hip_module_chain_waves(void* handle, int32_t n_waves);
 int vbn_hip_normalize_weights(const float* log_w, float* w, float* ess, int64_t n_queries,
                               int32_t n_samples, int32_t normalize, float eps, void* stream);
 
+/* (ABI v11) vbn_hip_normalize_weights with the importance-sampling fallback decision on the
+ * device (importance_sampling.py:82-88, no host round trip):
+ *   run_if: NULL, or a device flag -- when *run_if == 0 nothing is written (the normalisation of
+ *           the predicated likelihood-weighting re-draw, vbn_walk_args.run_if);
+ *   flag:   NULL, or a device int32 the caller zeroed: set to 1 when some query's ESS < ess_thr
+ *           (NaN ESS never sets it); needs normalize = 1. */
+int vbn_hip_normalize_weights_ex(const float* log_w, float* w, float* ess, int64_t n_queries, int32_t n_samples,
+                                 int32_t normalize, float eps, const int32_t* run_if, int32_t* flag, float ess_thr,
+                                 void* stream);
+
 /* Multinomial resampling of a segmented walk's particle state (resampled_importance_sampling.py
  * :33-41): per query b, S indices idx[s] ~ Categorical(w[b, :]) (inverse CDF of u[b][s] if u is
  * given, else counter-based Philox keyed by (seed, offset, query q_base + b, s)), then
@@ -124,6 +134,13 @@ int vbn_hip_posterior_stats(const float* pdf, const float* x, float* mean, float
  *   tensor: feature 0); w [B][S]; probs [B][k] float64; bad [B] int32. */
 int vbn_hip_discrete_posterior(const float* x, int64_t x_stride, const float* w, double* probs, int32_t* bad,
                                int64_t n_queries, int32_t n_samples, int32_t k, void* stream);
+
+/* (ABI v11) vbn_hip_discrete_posterior for float32 or float64 samples / weights (x_f64, w_f64:
+ * 0 = float32, 1 = float64).  The reference converts each element with float() before it bins
+ * or sums it, so a float64 input is binned and summed at its own precision. */
+int vbn_hip_discrete_posterior_typed(const void* x, int32_t x_f64, int64_t x_stride, const void* w, int32_t w_f64,
+                                     double* probs, int32_t* bad, int64_t n_queries, int32_t n_samples, int32_t k,
+                                     void* stream);
 
 /* Rao-Blackwellized target epilogue over P particles per query
  * (rao_blackwellized_marginalization.py:68-76, 255-317):

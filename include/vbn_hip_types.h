@@ -156,6 +156,10 @@ typedef struct vbn_walk_args {
                               no writes) and the MLPs run one 32-particle MFMA group   */
   const float* precomp_q;  /* (ABI v9) per-query quantities of the VBN_F_PRECOMP_Q steps
                               [B][stride] (read-only; lean walks, n_samples % 64 == 0), or NULL */
+  const int32_t* run_if;   /* (ABI v11) device flag or NULL: when *run_if == 0 every wave of the
+                              launch returns at once and nothing is written (the importance-
+                              sampling -> likelihood-weighting fallback, decided on the device
+                              without a host round trip)                                 */
 } vbn_walk_args;
 
 #endif /* VBN_HIP_TYPES_H */

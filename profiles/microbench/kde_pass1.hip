@@ -1,0 +1,343 @@
+// kde_pass1.hip -- instruction-mix variants of the KDE inverse-CDF pass 1 (MI355X, gfx950).
+//   hipcc -O3 -fno-slp-vectorize --offload-arch=gfx950 profiles/microbench/kde_pass1.hip -o /tmp/kde_pass1 && /tmp/kde_pass1
+// One wave64 = 64 particles of one KDE node; it sums exp2(<contraction>) over M = 10,240
+// points in 16 chunks, as vbn_walk_impl.h kde_index_mfma does, and writes its total.  65,536
+// one-wave workgroups (cfg4's 4096 x 1024 particles).  Variants:
+//   cur16     : the walk's kde_bf16_sums as of round 4 (16x16x32 bf16, 4 tiles of 16
+//               particles, f32x2 adds, operands rotated through a copy each trip)
+//   u16       : the same math, two trips per iteration with named operand sets (no copies)
+//   s16       : u16 with plain f32 adds (4 per tile and MFMA)
+//   s32       : v_mfma_f32_32x32x16_bf16, K = 16 (<= 2 features with the particle's |x'|^2
+//               factored out), 2 tiles of 32 particles, 16 exps per MFMA, plain f32 adds
+//   p32       : s32 with f32x2 adds
+//   s32k32    : K = 32 (3 features) as two chained 32x32x16 MFMAs per tile, plain adds
+// Prints ms per launch and pair rate against the v_exp_f32 issue peak (8 cycles per wave64
+// instruction and SIMD, 1024 SIMDs, 2.4 GHz = 19.66 T/s).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define CHECK(x)                                                              \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                \
+    }                                                                         \
+  } while (0)
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int CHUNKS = 16;
+// every variant at the walk's 4 waves per SIMD: 16 one-wave workgroups per CU share its 160 KiB of LDS
+constexpr int LDS_PER_WAVE = 10240;
+constexpr int M = 10240;                  // points (cfg4: 10,000 padded to the chunk grid)
+constexpr int NB16 = M / 16;              // 16-point blocks: 640, 40 per chunk
+constexpr int NB32 = M / 32;              // 32-point blocks: 320, 20 per chunk
+
+__device__ __forceinline__ bf16x8 bop(int lane, int t, float seed) {
+  bf16x8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (__bf16)(0.05f * (float)((lane * 7 + t * 3 + j) & 15) * seed);
+  return b;
+}
+
+__device__ __forceinline__ float reduce16(const float (&s)[4], int lane) {
+  const int h = lane >> 5, b = (lane >> 4) & 1;
+  float k0 = h ? s[2] : s[0], k1 = h ? s[3] : s[1];
+  const float o0 = h ? s[0] : s[2], o1 = h ? s[1] : s[3];
+  k0 += __shfl_xor(o0, 32);
+  k1 += __shfl_xor(o1, 32);
+  const float k = b ? k1 : k0, o = b ? k0 : k1;
+  return k + __shfl_xor(o, 16);
+}
+
+__device__ __forceinline__ float reduce32(const float (&s)[2], int lane) {
+  const int h = lane >> 5;
+  const float k = h ? s[1] : s[0], o = h ? s[0] : s[1];
+  return k + __shfl_xor(o, 32);
+}
+
+// ---- cur16: round 4's kde_bf16_sums ---------------------------------------------------------
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_cur16(const bf16x8* __restrict__ pack, float* out, float seed) {
+  const int lane = threadIdx.x;
+  bf16x8 ob[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ob[t] = bop(lane, t, seed);
+  const bf16x8* __restrict__ pa = pack + lane;
+  const int cb = NB16 / CHUNKS, blast = NB16 - 1;
+  bf16x8 nx[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) nx[u] = pa[min(u, blast) * 64];
+  double tot = 0.0;
+  for (int ch = 0; ch < CHUNKS; ++ch) {
+    f32x2 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x2{0.f, 0.f};
+    for (int b = ch * cb; b < ch * cb + cb; b += 4) {
+      const bf16x8 a[4] = {nx[0], nx[1], nx[2], nx[3]};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) nx[u] = pa[min(b + 4 + u, blast) * 64];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        f32x4 d[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          d[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], ob[t], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f32x2 e01 = f32x2{__builtin_amdgcn_exp2f(d[t][0]), __builtin_amdgcn_exp2f(d[t][1])};
+          const f32x2 e23 = f32x2{__builtin_amdgcn_exp2f(d[t][2]), __builtin_amdgcn_exp2f(d[t][3])};
+          acc[t] += e01 + e23;
+        }
+      }
+    }
+    float s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) s[t] = acc[t].x + acc[t].y;
+    tot += (double)reduce16(s, lane);
+  }
+  out[blockIdx.x * 64 + lane] = (float)tot;
+}
+
+// ---- u16 / s16: two trips per iteration, named operand sets ---------------------------------
+template <bool SCALAR>
+__device__ __forceinline__ void trip16(const bf16x8 (&a)[4], const bf16x8 (&ob)[4], float (&s)[4][2],
+                                       f32x2 (&acc)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    f32x4 d[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      d[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], ob[t], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float e0 = __builtin_amdgcn_exp2f(d[t][0]), e1 = __builtin_amdgcn_exp2f(d[t][1]);
+      const float e2 = __builtin_amdgcn_exp2f(d[t][2]), e3 = __builtin_amdgcn_exp2f(d[t][3]);
+      if (SCALAR) {
+        s[t][0] += e0; s[t][1] += e1; s[t][0] += e2; s[t][1] += e3;
+      } else {
+        acc[t] += f32x2{e0, e1} + f32x2{e2, e3};
+      }
+    }
+  }
+}
+
+template <bool SCALAR>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_u16(const bf16x8* __restrict__ pack, float* out, float seed) {
+  const int lane = threadIdx.x;
+  bf16x8 ob[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ob[t] = bop(lane, t, seed);
+  const bf16x8* __restrict__ pa = pack + lane;
+  const int cb = NB16 / CHUNKS, blast = NB16 - 1;      // cb a multiple of 8
+  bf16x8 xa[4], xb[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) xa[u] = pa[min(u, blast) * 64];
+  double tot = 0.0;
+  for (int ch = 0; ch < CHUNKS; ++ch) {
+    float s[4][2] = {{0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}, {0.f, 0.f}};
+    f32x2 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x2{0.f, 0.f};
+    for (int b = ch * cb; b < ch * cb + cb; b += 8) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xb[u] = pa[min(b + 4 + u, blast) * 64];
+      trip16<SCALAR>(xa, ob, s, acc);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xa[u] = pa[min(b + 8 + u, blast) * 64];
+      trip16<SCALAR>(xb, ob, s, acc);
+    }
+    float r[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) r[t] = SCALAR ? s[t][0] + s[t][1] : acc[t].x + acc[t].y;
+    tot += (double)reduce16(r, lane);
+  }
+  out[blockIdx.x * 64 + lane] = (float)tot;
+}
+
+// ---- s32 / p32: 32x32x16, 2 tiles of 32 particles -------------------------------------------
+template <bool SCALAR>
+__device__ __forceinline__ void trip32(const bf16x8 (&a)[4], const bf16x8 (&ob)[2], float (&s)[2][4],
+                                       f32x2 (&acc)[2][2]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    f32x16 d[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 z;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) z[i] = 0.f;
+      d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], ob[t], z, 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        const float e0 = __builtin_amdgcn_exp2f(d[t][i]), e1 = __builtin_amdgcn_exp2f(d[t][i + 1]);
+        const float e2 = __builtin_amdgcn_exp2f(d[t][i + 2]), e3 = __builtin_amdgcn_exp2f(d[t][i + 3]);
+        if (SCALAR) {
+          s[t][0] += e0; s[t][1] += e1; s[t][2] += e2; s[t][3] += e3;
+        } else {
+          acc[t][0] += f32x2{e0, e1};
+          acc[t][1] += f32x2{e2, e3};
+        }
+      }
+    }
+  }
+}
+
+template <bool SCALAR>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_s32(const bf16x8* __restrict__ pack, float* out, float seed) {
+  const int lane = threadIdx.x;
+  bf16x8 ob[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) ob[t] = bop(lane, t, seed);
+  const bf16x8* __restrict__ pa = pack + lane;
+  const int cb = NB32 / CHUNKS, blast = NB32 - 1;      // 20 blocks per chunk: trips of 4, pairs of trips
+  bf16x8 xa[4], xb[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) xa[u] = pa[min(u, blast) * 64];
+  double tot = 0.0;
+  for (int ch = 0; ch < CHUNKS; ++ch) {
+    float s[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x2 acc[2][2] = {{f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}};
+    const int b0 = ch * cb, b1 = b0 + cb;
+    int b = b0;
+    for (; b + 8 <= b1; b += 8) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xb[u] = pa[min(b + 4 + u, blast) * 64];
+      trip32<SCALAR>(xa, ob, s, acc);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xa[u] = pa[min(b + 8 + u, blast) * 64];
+      trip32<SCALAR>(xb, ob, s, acc);
+    }
+    if (b < b1) {                                       // a last single trip (cb = 20 = 2 x 8 + 4)
+      trip32<SCALAR>(xa, ob, s, acc);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xa[u] = pa[min(b + 4 + u, blast) * 64];
+    }
+    float r[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      r[t] = SCALAR ? (s[t][0] + s[t][1]) + (s[t][2] + s[t][3])
+                    : (acc[t][0].x + acc[t][0].y) + (acc[t][1].x + acc[t][1].y);
+    tot += (double)reduce32(r, lane);
+  }
+  out[blockIdx.x * 64 + lane] = (float)tot;
+}
+
+// ---- s32k32: K = 32 as two chained 32x32x16 per tile ----------------------------------------
+__device__ __forceinline__ void trip32k(const bf16x8 (&a)[4], const bf16x8 (&ob)[2][2], float (&s)[2][4]) {
+#pragma unroll
+  for (int u = 0; u < 4; u += 2) {
+    f32x16 d[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 z;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) z[i] = 0.f;
+      d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u], ob[t][0], z, 0, 0, 0);
+      d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[u + 1], ob[t][1], d[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        s[t][0] += __builtin_amdgcn_exp2f(d[t][i]);
+        s[t][1] += __builtin_amdgcn_exp2f(d[t][i + 1]);
+        s[t][2] += __builtin_amdgcn_exp2f(d[t][i + 2]);
+        s[t][3] += __builtin_amdgcn_exp2f(d[t][i + 3]);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_s32k32(const bf16x8* __restrict__ pack, float* out, float seed) {
+  const int lane = threadIdx.x;
+  bf16x8 ob[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) { ob[t][0] = bop(lane, t, seed); ob[t][1] = bop(lane, t + 2, seed); }
+  const bf16x8* __restrict__ pa = pack + lane;        // [block][K half][64 lanes]
+  const int cb = NB32 / CHUNKS, blast = 2 * NB32 - 1;
+  bf16x8 xa[4], xb[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) xa[u] = pa[min(u, blast) * 64];
+  double tot = 0.0;
+  for (int ch = 0; ch < CHUNKS; ++ch) {
+    float s[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const int h0 = 2 * ch * cb, h1 = h0 + 2 * cb;     // halves: 2 per block, 4 per trip (2 blocks)
+    int h = h0;
+    for (; h + 8 <= h1; h += 8) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xb[u] = pa[min(h + 4 + u, blast) * 64];
+      trip32k(xa, ob, s);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xa[u] = pa[min(h + 8 + u, blast) * 64];
+      trip32k(xb, ob, s);
+    }
+    if (h < h1) {
+      trip32k(xa, ob, s);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xa[u] = pa[min(h + 4 + u, blast) * 64];
+    }
+    float r[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) r[t] = (s[t][0] + s[t][1]) + (s[t][2] + s[t][3]);
+    tot += (double)reduce32(r, lane);
+  }
+  out[blockIdx.x * 64 + lane] = (float)tot;
+}
+
+static unsigned short bf16_bits(float v) {
+  unsigned u;
+  memcpy(&u, &v, 4);
+  return (unsigned short)(u >> 16);
+}
+
+int main() {
+  const int waves = 65536;
+  const size_t n_pack = (size_t)NB16 * 64 * 8;       // bf16 elements: M points x 32 slots
+  unsigned short* h = (unsigned short*)malloc(n_pack * 2);
+  srand(1);
+  for (size_t i = 0; i < n_pack; ++i) h[i] = bf16_bits(-0.5f + (float)rand() / RAND_MAX);
+  void* pack;
+  float* out;
+  CHECK(hipMalloc(&pack, n_pack * 2));
+  CHECK(hipMalloc(&out, (size_t)waves * 64 * 4));
+  CHECK(hipMemcpy(pack, h, n_pack * 2, hipMemcpyHostToDevice));
+  const bf16x8* p = (const bf16x8*)pack;
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  struct V { const char* name; void (*fn)(const bf16x8*, float*, float); };
+  V vs[] = {{"cur16", k_cur16}, {"u16", k_u16<false>}, {"s16", k_u16<true>},
+            {"s32", k_s32<true>}, {"p32", k_s32<false>}, {"s32k32", k_s32k32}};
+  const double pairs = (double)waves * 64 * M;
+  const double peak = 8.0 * 1024 * 2.4e9;
+  for (int rep = 0; rep < 2; ++rep) {
+    for (auto& v : vs) {
+      for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(v.fn, dim3(waves), dim3(64), LDS_PER_WAVE, 0, p, out, 1.0f + i);
+      CHECK(hipEventRecord(e0, 0));
+      const int n = 10;
+      for (int i = 0; i < n; ++i) hipLaunchKernelGGL(v.fn, dim3(waves), dim3(64), LDS_PER_WAVE, 0, p, out, 1.0f + i);
+      CHECK(hipEventRecord(e1, 0));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= n;
+      const double rate = pairs / (ms * 1e-3);
+      printf("{\"variant\": \"%s\", \"rep\": %d, \"ms\": %.4f, \"Tpairs_s\": %.3f, \"frac_exp_peak\": %.4f}\n",
+             v.name, rep, ms, rate / 1e12, rate / peak);
+      fflush(stdout);
+    }
+  }
+  float hs[4];
+  CHECK(hipMemcpy(hs, out, 16, hipMemcpyDeviceToHost));
+  printf("# out[0..3] %g %g %g %g\n", hs[0], hs[1], hs[2], hs[3]);
+  return 0;
+}

@@ -66,6 +66,22 @@ def main():
             pdf, xs = outs
             res[name] = {"seeds": seeds, "fallback": bool(getattr(sh.engine, "_last_fallback", False)),
                          "pdf": None if pdf is None else pdf.cpu(), "xs": None if xs is None else xs.cpu()}
+        # VBN.precompile behind a ShardedEngine: builds the local plan with no
+        # collective and leaves the sharded call counter and the torch RNG alone, so the two
+        # calls after it see the seeds of the "mcm" case above
+        from vectorizedbayesiannetwork_amd.engines import MonteCarloMarginalization
+        torch.manual_seed(1000 + a.rank)
+        sh = ShardedEngine(MonteCarloMarginalization(n_samples=S), gather=True)
+        vbn._inference = sh
+        st = vbn.precompile([{"target": target, "evidence": sorted(ev)}])
+        seeds = []
+        for _ in range(2):
+            pdf, xs = vbn.infer_posterior(Query(target, {k: v.cuda() for k, v in ev.items()}))
+            seeds.append(sh.last_seed)
+        torch.cuda.synchronize()
+        vbn._inference = None
+        res["mcm_precompiled"] = {"seeds": seeds, "fallback": False, "plans": st["plans"],
+                                  "pdf": None if pdf is None else pdf.cpu(), "xs": None if xs is None else xs.cpu()}
         torch.manual_seed(1000 + a.rank)
         sh = ShardedEngine(AncestralSampler(n_samples=S), gather=True)
         xs = sh.sample(vbn, Query(target, {k: v.cuda() for k, v in ev.items()}), S)

@@ -66,6 +66,15 @@ def _cases():
     s = torch.randint(0, 8, (300, 256), generator=g).float()
     w = torch.rand(300, 256, generator=g)
     add("batch300", s, w, 8)
+    # float64 inputs: half-integers off by 1e-12 bin by their own value (a float32
+    # cast would round them onto the half and to even), weights 1 + O(1e-12) sum in float64
+    base = torch.randint(0, 6, (3, 800), generator=g).double() + 0.5
+    off = torch.where(torch.rand(3, 800, generator=g, dtype=torch.float64) < 0.5, 1e-12, -1e-12)
+    w = 1.0 + torch.rand(3, 800, generator=g, dtype=torch.float64) * 1e-12
+    add("f64_both", base + off, w, 6)
+    add("f64_samples_f32_weights", base - off, torch.rand(3, 800, generator=g), 6)
+    add("f32_samples_f64_weights", torch.randint(0, 4, (2, 500), generator=g).float(),
+        torch.rand(2, 500, generator=g, dtype=torch.float64) * 1e-300, 4)
     return out
 
 

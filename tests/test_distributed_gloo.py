@@ -52,6 +52,17 @@ def _expected_seed(calls: int = 1) -> int:
     return seed
 
 
+def _val(t):
+    """A tensor sent through an mp.Queue by value: torch pickles tensors as shared-memory fds
+    served by the sending process, which may have exited before the parent unpickles (a
+    ConnectionResetError); numpy arrays pickle their bytes."""
+    return None if t is None else t.detach().cpu().numpy().copy()
+
+
+def _ten(a):
+    return None if a is None else torch.from_numpy(a)
+
+
 def _rendezvous():
     """A fresh file:// rendezvous for one world (no TCP port to race for between tests)."""
     return "file://" + os.path.join(tempfile.mkdtemp(prefix="vbn_gloo_"), "store")
@@ -65,8 +76,7 @@ def _worker(rank, world, init, ev, out_q, calls=1, overlap=False):
         for _ in range(calls):                        # later calls: no collective for the seed
             pdf, xs = eng.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}))
         eng.wait()
-        out_q.put((rank, None if pdf is None else pdf.clone(), None if xs is None else xs.clone(),
-                   eng.engine.last_fallback))
+        out_q.put((rank, _val(pdf), _val(xs), eng.engine.last_fallback))
     finally:
         dist.destroy_process_group()
 
@@ -81,7 +91,7 @@ def _run(ev, world=2, calls=1, overlap=False):
     res = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
-    return sorted(res, key=lambda r: r[0])
+    return sorted([(r, _ten(a), _ten(b), fb) for r, a, b, fb in res], key=lambda r: r[0])
 
 
 @pytest.mark.parametrize("ragged", [False, True])
@@ -145,7 +155,7 @@ def _chain_worker(rank, world, init, ev, out_q):
         torch.manual_seed(123 + rank)
         eng = ShardedEngine(StubChainSampler(), gather=True)
         xs = eng.sample(None, Query(target="y", evidence={"x": ev}, do={}), 5)
-        out_q.put((rank, None if xs is None else xs.clone()))
+        out_q.put((rank, _val(xs)))
     finally:
         dist.destroy_process_group()
 
@@ -163,6 +173,7 @@ def test_gloo_world2_sharded_chains_match_single_process():
     for p in procs:
         p.join(timeout=60)
     (_, xs), (_, xs1) = res
+    xs = _ten(xs)
     assert xs1 is None
     seed = _expected_seed()
     ref = StubChainSampler().sample(None, Query(target="y", evidence={"x": ev}, do={}), 5, seed=seed)
@@ -216,7 +227,7 @@ def _seeded_worker(rank, world, init, ev, out_q, calls):
             pending.append(len(eng._pending))
             if pdf is not None:
                 eng.wait()
-                outs.append(pdf.clone())
+                outs.append(_val(pdf))
         out_q.put((rank, outs, pending, eng.gather_bytes))
     finally:
         dist.destroy_process_group()
@@ -241,7 +252,7 @@ def test_gloo_sharded_engine_keeps_a_seeded_engines_sequence():
     ref = SeededStub(4242)
     for k in range(calls):
         rpdf, _ = ref.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}), seed=ref._seed({}))
-        assert torch.equal(outs[k], rpdf)
+        assert torch.equal(_ten(outs[k]), rpdf)
     assert outs1 == [] and max(pending1) <= 2, pending1           # one call (pdf + samples) in flight
     shard = 4 * S * 4 + 4 * S * 1 * 4                 # pdf [4, S] + samples [4, S, 1] fp32 from rank 1
     assert nbytes == calls * shard

@@ -107,3 +107,15 @@ def test_two_ranks_match_single_process(rank_results, name):
     assert torch.equal(r0["xs"], xs), f"{name}: gathered samples differ from the single-process batch"
     if pdf is not None:
         assert torch.equal(r0["pdf"], pdf), f"{name}: gathered pdf/weights differ from the single-process batch"
+
+
+def test_precompile_behind_sharded_engine(rank_results):
+    """VBN.precompile with a ShardedEngine as the inference method (world 2, one-query dummy
+    batch): plans built on each rank with no collective, and the sharded calls after it get the
+    same seeds and outputs as without the precompile (the "mcm" case)."""
+    r0, r1 = rank_results[0]["mcm_precompiled"], rank_results[1]["mcm_precompiled"]
+    assert r0["plans"] >= 1 and r1["plans"] >= 1
+    assert r0["seeds"] == r1["seeds"] == rank_results[0]["mcm"]["seeds"]
+    assert r1["xs"] is None
+    assert torch.equal(r0["xs"], rank_results[0]["mcm"]["xs"])
+    assert torch.equal(r0["pdf"], rank_results[0]["mcm"]["pdf"])

@@ -201,3 +201,22 @@ def test_precompile_signatures_ahead_of_time():
     torch.cuda.synchronize()
     assert ops.LAST_WALK.get("specialised")
     assert torch.isfinite(xs).all()
+
+
+def test_precompile_leaves_seed_sequences_alone():
+    """precompile builds plans without drawing seeds -- a seeded engine's first call
+    after it equals a fresh engine's first call bit for bit, and an unseeded engine's precompile
+    leaves the global torch RNG where it was."""
+    vbn, q = _fresh_workload(9303, B)
+    vbn.set_inference_method("monte_carlo_marginalization", n_samples=S, seed=77)
+    vbn.precompile([{"target": q.target, "evidence": list(q.evidence)}])
+    w1, x1 = vbn.infer_posterior(q)
+    vbn2, q2 = _fresh_workload(9303, B)
+    vbn2.set_inference_method("monte_carlo_marginalization", n_samples=S, seed=77)
+    w2, x2 = vbn2.infer_posterior(q2)
+    torch.cuda.synchronize()
+    assert torch.equal(w1, w2) and torch.equal(x1, x2)
+    vbn.set_inference_method("monte_carlo_marginalization", n_samples=S)
+    state = torch.get_rng_state()
+    vbn.precompile([{"target": q.target, "evidence": list(q.evidence)}])
+    assert torch.equal(state, torch.get_rng_state())

@@ -90,3 +90,18 @@ def test_box_muller_pairs_follow_the_table():
             from philox_draws import box_muller_pair
             assert torch.equal(b.reshape(-1), torch.from_numpy(box_muller_pair(w0, w1)[1]))
             break
+
+
+def test_lds_bound_counts_staged_weight_buffers():
+    """a gaussian_nn plan whose value slots alone fit 16 waves per CU but whose two
+    staged weight buffers (walk_shape in csrc/vbn_walk.hip) do not is LDS-bound; the same plan
+    in an unstaged kind set (a KDE node) is not."""
+    from types import SimpleNamespace
+    from vectorizedbayesiannetwork_amd import engines as E
+    p = SimpleNamespace(n_slots=20, max_out=2, kind_mask=1, wbuf=8192)
+    assert (p.n_slots + p.max_out) * 64 * 4 * 16 <= 160 * 1024          # slots alone: 16 waves
+    assert E._resident_waves(p) == 4 and E._lds_bound(p)                # 2 x 32 KiB per workgroup
+    p.wbuf = 256
+    assert E._resident_waves(p) == 16 and not E._lds_bound(p)
+    p.kind_mask, p.wbuf = 1 | 8, 8192                                   # kde: weights read from the blob
+    assert E._resident_waves(p) == 16 and not E._lds_bound(p)

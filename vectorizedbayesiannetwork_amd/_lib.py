@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -20,10 +20,12 @@ EXPORTS = (
     "vbn_hip_last_error",
     "vbn_hip_walk",
     "vbn_hip_normalize_weights",
+    "vbn_hip_normalize_weights_ex",
     "vbn_hip_rb_epilogue",
     "vbn_hip_resample",
     "vbn_hip_posterior_stats",
     "vbn_hip_discrete_posterior",
+    "vbn_hip_discrete_posterior_typed",
     "vbn_hip_lds_bytes",
     "vbn_hip_struct_size",
     "vbn_hip_walk_kind_set",
@@ -70,6 +72,7 @@ class VbnWalkArgs(ctypes.Structure):
         ("wbuf_floats", ctypes.c_int32),
         ("wave_particles", ctypes.c_int32),
         ("precomp_q", ctypes.c_void_p),
+        ("run_if", ctypes.c_void_p),
     ]
 
 
@@ -107,6 +110,10 @@ def load(path: str = None) -> ctypes.CDLL:
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
             ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
         lib.vbn_hip_normalize_weights.restype = ctypes.c_int
+        lib.vbn_hip_normalize_weights_ex.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+            ctypes.c_int32, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p]
+        lib.vbn_hip_normalize_weights_ex.restype = ctypes.c_int
         lib.vbn_hip_rb_epilogue.argtypes = [
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -124,6 +131,10 @@ def load(path: str = None) -> ctypes.CDLL:
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
         lib.vbn_hip_discrete_posterior.restype = ctypes.c_int
+        lib.vbn_hip_discrete_posterior_typed.argtypes = [
+            ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+        lib.vbn_hip_discrete_posterior_typed.restype = ctypes.c_int
         lib.vbn_hip_lds_bytes.argtypes = [ctypes.c_int32, ctypes.c_int32]
         lib.vbn_hip_lds_bytes.restype = ctypes.c_int64
         lib.vbn_hip_walk_kind_set.argtypes = [ctypes.POINTER(VbnWalkArgs)]

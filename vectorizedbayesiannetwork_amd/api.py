@@ -130,6 +130,12 @@ def _resolve(method, registry, kind: str, kwargs):
     raise TypeError("method must be a string, ConfigItem, or callable")
 
 
+def _local_engine(engine):
+    """The engine a ShardedEngine wraps (distributed.py), else the engine itself."""
+    from .distributed import ShardedEngine
+    return engine.engine if isinstance(engine, ShardedEngine) else engine
+
+
 class VBN:
     """Accelerated VBN: same inference/sampling surface, GPU execution."""
 
@@ -275,17 +281,21 @@ class VBN:
             methods.append("sample")
         if not methods:
             raise RuntimeError("Call set_inference_method(...) or set_sampling_method(...) before precompile().")
+        # the local engines build the plans: a ShardedEngine's collectives (seed broadcast,
+        # gathers) and its call counter stay untouched, and an explicit seed keeps a seeded
+        # engine's sequence and the global torch RNG where they were
+        infer, samp = _local_engine(self._inference), _local_engine(self._sampling)
         for sig in signatures:
             names = {k: list(sig.get(k) or []) for k in ("evidence", "do")}
-            q = {"target": sig.get("target") or sig.get("target_feature"),
-                 "evidence": {n: torch.zeros(1, self.model.out_dim(n)) for n in names["evidence"]},
-                 "do": {n: torch.zeros(1, self.model.out_dim(n)) for n in names["do"]}}
+            q = self._normalize_query({"target": sig.get("target") or sig.get("target_feature"),
+                                       "evidence": {n: torch.zeros(1, self.model.out_dim(n)) for n in names["evidence"]},
+                                       "do": {n: torch.zeros(1, self.model.out_dim(n)) for n in names["do"]}})
             kw = {} if n_samples is None else {"n_samples": int(n_samples)}
             with E.precompile_mode("background" if background else "sync") as st:
                 if "infer" in methods:
-                    self.infer_posterior(q, **kw)
+                    infer.infer_posterior(self, q, seed=0, **kw)
                 if "sample" in methods:
-                    self.sample(q, **({} if n_samples is None else {"n_samples": int(n_samples)}))
+                    samp.sample(self, q, n_samples=200 if n_samples is None else int(n_samples), seed=0)
             out["plans"] += st["plans"]
             out["ready"] += st["ready"]
         return out
@@ -312,9 +322,9 @@ class VBN:
                                    "do": {n: torch.zeros(1, self.model.out_dim(n)) for n in names["do"]}})
         with E.precompile_mode("none") as st:
             if method == "ancestral":
-                SAMPLING_REGISTRY[method](n_samples=n_samples, **method_kwargs).sample(self, q, n_samples)
+                SAMPLING_REGISTRY[method](n_samples=n_samples, **method_kwargs).sample(self, q, n_samples, seed=0)
             else:
-                INFERENCE_REGISTRY[method](n_samples=n_samples, **method_kwargs).infer_posterior(self, q)
+                INFERENCE_REGISTRY[method](n_samples=n_samples, **method_kwargs).infer_posterior(self, q, seed=0)
         seen = st["seen"]
         if not seen:
             raise RuntimeError("pack_query: the engine launched no walk for this signature")

@@ -25,8 +25,14 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// run_if (ABI v11): when non-NULL and *run_if == 0 the launch writes nothing (the predicated
+// fallback normalisation).  flag: when non-NULL, set to 1 (atomic OR) by every query whose
+// ESS < ess_thr (a NaN ESS never sets it; importance_sampling.py:85-86); the caller zeroes it.
 __global__ void __launch_bounds__(NW_THREADS) vbn_normalize_kernel(const float* log_w, float* w, float* ess,
-                                                                  int S, int normalize, float eps) {
+                                                                  int S, int normalize, float eps,
+                                                                  const int32_t* run_if, int32_t* flag,
+                                                                  float ess_thr) {
+  if (run_if && *run_if == 0) return;
   __shared__ float red[NW_THREADS / WAVE];
   __shared__ int nan_flag;
   const int64_t row = blockIdx.x;
@@ -77,7 +83,9 @@ __global__ void __launch_bounds__(NW_THREADS) vbn_normalize_kernel(const float* 
   if (tid == 0) {
     float t = 0.f;
     for (int k = 0; k < NW_THREADS / WAVE; ++k) t += red[k];
-    if (ess) ess[row] = 1.0f / t;
+    const float e = 1.0f / t;
+    if (ess) ess[row] = e;
+    if (flag && e < ess_thr) atomicOr(flag, 1);
   }
 }
 
@@ -326,9 +334,11 @@ __device__ double np_pairwise_sum(const double* a, int64_t n, int64_t st) {
   return np_pairwise_sum<(D > 0 ? D - 1 : 0)>(a, n2, st) + np_pairwise_sum<(D > 0 ? D - 1 : 0)>(a + n2 * st, n - n2, st);
 }
 
-template <bool LDS_BINS>
+// TX / TW: the samples' / weights' element type (float or double: the reference converts each
+// with float(), so a float64 input bins and sums its own values, with no float32 rounding)
+template <bool LDS_BINS, class TX, class TW>
 __global__ void __launch_bounds__(DP_THREADS) vbn_discrete_posterior_kernel(
-    const float* __restrict__ x, int64_t x_stride, const float* __restrict__ w, double* __restrict__ probs,
+    const TX* __restrict__ x, int64_t x_stride, const TW* __restrict__ w, double* __restrict__ probs,
     int32_t* __restrict__ bad, int64_t B, int S, int k) {
 #pragma clang fp contract(off)
   extern __shared__ double bins_lds[];
@@ -337,13 +347,13 @@ __global__ void __launch_bounds__(DP_THREADS) vbn_discrete_posterior_kernel(
   double* h = LDS_BINS ? bins_lds + threadIdx.x : probs + b * k;
   const int64_t hs = LDS_BINS ? DP_THREADS : 1;
   for (int c = 0; c < k; ++c) h[c * hs] = 0.0;
-  const float* xr = x + b * (int64_t)S * x_stride;
-  const float* wr = w + b * (int64_t)S;
+  const TX* xr = x + b * (int64_t)S * x_stride;
+  const TW* wr = w + b * (int64_t)S;
   int flag = 0;
   for (int s = 0; s < S; ++s) {
-    const float wt = wr[s];
+    const TW wt = wr[s];
     if (!__builtin_isfinite(wt)) continue;
-    const float v = xr[(int64_t)s * x_stride];
+    const TX v = xr[(int64_t)s * x_stride];
     if (!__builtin_isfinite(v)) {
       flag = v != v ? 1 : 2;
       break;
@@ -593,22 +603,43 @@ extern "C" int vbn_hip_posterior_stats(const float* pdf, const float* x, float* 
   return 0;
 }
 
-extern "C" int vbn_hip_discrete_posterior(const float* x, int64_t x_stride, const float* w, double* probs,
-                                          int32_t* bad, int64_t n_queries, int32_t n_samples, int32_t k,
-                                          void* stream) {
-  if (!x || !w || !probs || !bad || x_stride <= 0 || n_queries <= 0 || n_samples <= 0 || k <= 0)
-    return fail(VBN_E_ARGS, "vbn_hip_discrete_posterior: bad arguments");
+template <class TX, class TW>
+static void launch_discrete_posterior(const void* x, int64_t x_stride, const void* w, double* probs, int32_t* bad,
+                                      int64_t n_queries, int32_t n_samples, int32_t k, void* stream) {
   const unsigned grid = (unsigned)((n_queries + DP_THREADS - 1) / DP_THREADS);
   if (k <= DP_LDS_BINS)
-    hipLaunchKernelGGL(vbn_discrete_posterior_kernel<true>, dim3(grid), dim3(DP_THREADS),
-                       (size_t)k * DP_THREADS * sizeof(double), (hipStream_t)stream, x, x_stride, w, probs, bad,
-                       n_queries, n_samples, k);
+    hipLaunchKernelGGL((vbn_discrete_posterior_kernel<true, TX, TW>), dim3(grid), dim3(DP_THREADS),
+                       (size_t)k * DP_THREADS * sizeof(double), (hipStream_t)stream, (const TX*)x, x_stride,
+                       (const TW*)w, probs, bad, n_queries, n_samples, k);
   else
-    hipLaunchKernelGGL(vbn_discrete_posterior_kernel<false>, dim3(grid), dim3(DP_THREADS), 0, (hipStream_t)stream,
-                       x, x_stride, w, probs, bad, n_queries, n_samples, k);
+    hipLaunchKernelGGL((vbn_discrete_posterior_kernel<false, TX, TW>), dim3(grid), dim3(DP_THREADS), 0,
+                       (hipStream_t)stream, (const TX*)x, x_stride, (const TW*)w, probs, bad, n_queries, n_samples,
+                       k);
+}
+
+extern "C" int vbn_hip_discrete_posterior_typed(const void* x, int32_t x_f64, int64_t x_stride, const void* w,
+                                                int32_t w_f64, double* probs, int32_t* bad, int64_t n_queries,
+                                                int32_t n_samples, int32_t k, void* stream) {
+  if (!x || !w || !probs || !bad || x_stride <= 0 || n_queries <= 0 || n_samples <= 0 || k <= 0 ||
+      (x_f64 != 0 && x_f64 != 1) || (w_f64 != 0 && w_f64 != 1))
+    return fail(VBN_E_ARGS, "vbn_hip_discrete_posterior: bad arguments");
+  if (x_f64 && w_f64)
+    launch_discrete_posterior<double, double>(x, x_stride, w, probs, bad, n_queries, n_samples, k, stream);
+  else if (x_f64)
+    launch_discrete_posterior<double, float>(x, x_stride, w, probs, bad, n_queries, n_samples, k, stream);
+  else if (w_f64)
+    launch_discrete_posterior<float, double>(x, x_stride, w, probs, bad, n_queries, n_samples, k, stream);
+  else
+    launch_discrete_posterior<float, float>(x, x_stride, w, probs, bad, n_queries, n_samples, k, stream);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;
+}
+
+extern "C" int vbn_hip_discrete_posterior(const float* x, int64_t x_stride, const float* w, double* probs,
+                                          int32_t* bad, int64_t n_queries, int32_t n_samples, int32_t k,
+                                          void* stream) {
+  return vbn_hip_discrete_posterior_typed(x, 0, x_stride, w, 0, probs, bad, n_queries, n_samples, k, stream);
 }
 
 extern "C" int vbn_hip_resample(const float* w, const float* u, uint64_t seed, uint64_t offset, int64_t q_base,
@@ -642,13 +673,20 @@ extern "C" int vbn_hip_rb_epilogue(const float* log_w, const float* params, int6
   return 0;
 }
 
-extern "C" int vbn_hip_normalize_weights(const float* log_w, float* w, float* ess, int64_t n_queries,
-                                         int32_t n_samples, int32_t normalize, float eps, void* stream) {
-  if (!log_w || !w || n_queries <= 0 || n_samples <= 0)
+extern "C" int vbn_hip_normalize_weights_ex(const float* log_w, float* w, float* ess, int64_t n_queries,
+                                            int32_t n_samples, int32_t normalize, float eps, const int32_t* run_if,
+                                            int32_t* flag, float ess_thr, void* stream) {
+  if (!log_w || !w || n_queries <= 0 || n_samples <= 0 || (flag && !normalize))
     return fail(VBN_E_ARGS, "vbn_hip_normalize_weights: bad arguments");
   hipLaunchKernelGGL(vbn_normalize_kernel, dim3((unsigned)n_queries), dim3(NW_THREADS), 0,
-                     (hipStream_t)stream, log_w, w, ess, n_samples, normalize, eps);
+                     (hipStream_t)stream, log_w, w, ess, n_samples, normalize, eps, run_if, flag, ess_thr);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;
+}
+
+extern "C" int vbn_hip_normalize_weights(const float* log_w, float* w, float* ess, int64_t n_queries,
+                                         int32_t n_samples, int32_t normalize, float eps, void* stream) {
+  return vbn_hip_normalize_weights_ex(log_w, w, ess, n_queries, n_samples, normalize, eps, nullptr, nullptr, 0.f,
+                                      stream);
 }

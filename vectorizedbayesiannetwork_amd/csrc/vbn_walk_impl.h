@@ -1982,6 +1982,7 @@ template <unsigned KM>
 __global__ void __launch_bounds__(WG_MAX_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(VBN_WPE)))
 vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const vbn_step* __restrict__ steps,
                 const int32_t* __restrict__ in_cols) {
+  if (A.run_if && *A.run_if == 0) return;            // predicated launch, not needed (uniform)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6;
   const int per_wave = (A.n_slots + (A.max_out > 0 ? A.max_out : 1)) * WAVE;

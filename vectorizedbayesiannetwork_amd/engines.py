@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import threading
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -149,9 +150,27 @@ WAVES_PER_CU = 16                    # 4 waves per SIMD at the walk's 128-VGPR b
 ORDER_RESTARTS = 64                  # seeded restarts of the liveness greedy (<= ~0.4 s per plan build)
 
 
+def _resident_waves(p: QueryPlan) -> int:
+    """Waves per CU the walk's launch shape gives a full-size launch of plan ``p`` (walk_shape in
+    csrc/vbn_walk.hip): per-wave LDS vbn_hip_lds_bytes(n_slots, max_out), plus, for the kind sets
+    that stage MLP weights in LDS (only gaussian_nn / linear_gaussian, no generic MLP shapes:
+    staged_kinds), two weight buffers of ``wbuf`` floats per workgroup of 4, 2 or 1 waves."""
+    per_wave = (p.n_slots + max(p.max_out, 1)) * 64 * 4
+    staged = (p.kind_mask & 28) == 0 and not (p.kind_mask & 512)
+    best = 0
+    for w in ((4, 2, 1) if staged else (1,)):
+        lds = w * per_wave + (2 * p.wbuf * 4 if staged else 0)
+        if lds <= 160 * 1024:
+            best = max(best, min(WAVES_PER_CU, (160 * 1024 // lds) * w))
+    if staged and best == 0:                     # walk_shape falls back to an unstaged kind set
+        best = min(WAVES_PER_CU, 160 * 1024 // per_wave)
+    return best
+
+
 def _lds_bound(p: QueryPlan) -> bool:
-    """the plan's per-wave LDS (vbn_hip_lds_bytes) holds fewer than WAVES_PER_CU waves per CU"""
-    return (p.n_slots + max(p.max_out, 1)) * 64 * 4 * WAVES_PER_CU > 160 * 1024
+    """LDS (value slots, scratch rows and staged weight buffers) holds fewer than WAVES_PER_CU
+    waves of the plan per CU"""
+    return _resident_waves(p) < WAVES_PER_CU
 
 
 # per-sample / per-query precompute (plan.precompute_plans) in production walks; False: every
@@ -186,6 +205,15 @@ def _fixed_buffer(plan: QueryPlan, vals: Dict[str, torch.Tensor], rows: int, dev
     return torch.cat(cols, dim=1).contiguous()
 
 
+def _has_discrete(pk: PackedModel, nodes: Sequence[str]) -> bool:
+    """some node of ``nodes`` is a softmax_nn with discrete dims (its evidence is checked)"""
+    for n in nodes:
+        rec = pk.model.cpds[n]
+        if rec.kind == "softmax_nn" and bool(rec.state["_is_discrete"].bool().any()):
+            return True
+    return False
+
+
 def _check_discrete(pk: PackedModel, vals: Dict[str, torch.Tensor], nodes: Sequence[str]) -> None:
     """softmax_nn discrete dims reject values outside the class set (softmax_nn.py:622-625)."""
     for n in nodes:
@@ -209,8 +237,16 @@ def _next_seed() -> int:
 # last walk launched (introspection for bench.py's per-kernel timing)
 LAST_LAUNCH: Dict[str, object] = {}
 
-# VBN.precompile: engines build their plans and compile the specialised walks without launching
-_PRECOMPILE: Dict[str, object] = {"on": False, "compile": "sync", "plans": 0, "ready": 0}
+# VBN.precompile: engines build their plans and compile the specialised walks without launching.
+# Per thread: a precompile in one thread must not turn another thread's launches into no-ops.
+_PC_LOCAL = threading.local()
+
+
+def _pc_state() -> Dict[str, object]:
+    st = getattr(_PC_LOCAL, "state", None)
+    if st is None:
+        st = _PC_LOCAL.state = {"on": False, "compile": "sync", "plans": 0, "ready": 0}
+    return st
 
 
 @contextlib.contextmanager
@@ -219,15 +255,16 @@ def precompile_mode(compile: str = "sync"):
     nothing) the walk each engine call would launch, records its plan and returns zero outputs
     instead of launching it.  Yields a dict that holds, after the block, "plans" (walks seen),
     "ready" (their specialised modules loaded) and "seen" (the plans)."""
-    prev = dict(_PRECOMPILE)
+    pc = _pc_state()
+    prev = dict(pc)
     res: Dict[str, object] = {}
-    _PRECOMPILE.update(on=True, compile=compile, plans=0, ready=0, seen=[])
+    pc.update(on=True, compile=compile, plans=0, ready=0, seen=[])
     try:
         yield res
     finally:
-        res.update(plans=_PRECOMPILE["plans"], ready=_PRECOMPILE["ready"], seen=list(_PRECOMPILE["seen"]))
-        _PRECOMPILE.clear()
-        _PRECOMPILE.update(prev)
+        res.update(plans=pc["plans"], ready=pc["ready"], seen=list(pc["seen"]))
+        pc.clear()
+        pc.update(prev)
 
 
 def noise_tensor(pk: PackedModel, plan: QueryPlan, noise: Dict[str, Tuple], b: int, n: int) -> torch.Tensor:
@@ -288,10 +325,14 @@ def _side_stream(device: torch.device):
 def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: int, *,
              seed: int, offset: int = 0, q_base: int = 0, noise=None,
              fixed_per_particle: bool = False, state: Optional[torch.Tensor] = None, state_flags: int = 0,
-             step_begin: int = 0, step_end: int = -1, plan_jit: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
+             step_begin: int = 0, step_end: int = -1, plan_jit: int = 1, run_if: Optional[torch.Tensor] = None,
+             out_x: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """One launch of the particle walk; returns (lp [b,n] or empty, x [b,n,n_out_cols]).
     ``state``/``state_flags``/``step_begin``/``step_end``: one segment of a split walk;
-    ``plan_jit``: ops.walk (0 interpreter, 1 plan-specialised for large lean launches, 2 always)."""
+    ``plan_jit``: ops.walk (0 interpreter, 1 plan-specialised for large lean launches, 2 always);
+    ``run_if``: device int32 [1] predicating every launch (pre-passes included; nothing runs and
+    nothing is written when it holds 0); ``out_x``: samples written into this [b, n, n_out_cols]
+    tensor (a predicated launch that does not run leaves it as it was)."""
     n_out_cols = int(plan.out_cols.numel()) if plan.out_nodes else 0
     noise_b = 1
     if isinstance(noise, dict):
@@ -308,19 +349,20 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
     pre_ran = False
     use_pc = (PRECOMPUTE and plan.pc is not None and noise is None and state is None and step_begin == 0
               and step_end < 0 and n % 64 == 0 and not fixed_per_particle)
-    if _PRECOMPILE["on"]:
+    pcs = _pc_state()
+    if pcs["on"]:
         # VBN.precompile / pack_query: compile (or load) the specialised walk this launch would
         # run, record its plan, no launch
-        _PRECOMPILE.setdefault("seen", []).append(plan)
-        if state is None and noise is None and plan_jit and _PRECOMPILE["compile"] != "none":
+        pcs.setdefault("seen", []).append(plan)
+        if state is None and noise is None and plan_jit and pcs["compile"] != "none":
             from . import jit
             wp = plan.pc if use_pc else plan
             km = jit.walk_kind_set(wp, b, n, precomp=use_pc and plan.pre is not None)
             host = wp.steps._vbn_host
             dev = pk.device.index if pk.device.index is not None else 0
-            if jit.module_for(host[0], host[1], km, dev, host[2], compile=_PRECOMPILE["compile"]) is not None:
-                _PRECOMPILE["ready"] += 1
-            _PRECOMPILE["plans"] += 1
+            if jit.module_for(host[0], host[1], km, dev, host[2], compile=pcs["compile"]) is not None:
+                pcs["ready"] += 1
+            pcs["plans"] += 1
         lp = torch.zeros(b, n, device=pk.device) if plan.mode != MODE_SAMPLE else torch.empty(0, device=pk.device)
         return lp, torch.zeros(b, n, n_out_cols, device=pk.device)
     if use_pc:
@@ -337,10 +379,12 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
             side.wait_stream(main)
         if plan.pre is not None:
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                _, precomp = run_walk(pk, plan.pre, fixed, 1, n, seed=seed, offset=offset, plan_jit=0)
+                _, precomp = run_walk(pk, plan.pre, fixed, 1, n, seed=seed, offset=offset, plan_jit=0,
+                                      run_if=run_if)
             precomp = precomp.view(n, -1)
         if plan.pre_q is not None:
-            _, pq = run_walk(pk, plan.pre_q, fixed, b, 64, seed=seed, offset=offset, q_base=q_base, plan_jit=0)
+            _, pq = run_walk(pk, plan.pre_q, fixed, b, 64, seed=seed, offset=offset, q_base=q_base, plan_jit=0,
+                             run_if=run_if)
             precomp_q = _query_rows(pq, b, plan.pc.steps)
         if side is not None:
             main.wait_stream(side)
@@ -356,7 +400,8 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
             plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
             len(plan.noise_nodes), pk.dmax, n_out_cols, plan.mode, q_base, seed, offset,
             plan.mode != MODE_SAMPLE, plan.kind_mask)
-    gens = _generations(plan, b, n) if (state is None and noise is None and not fixed_per_particle) else 1
+    gens = (_generations(plan, b, n) if (state is None and noise is None and not fixed_per_particle
+                                          and run_if is None and out_x is None) else 1)
     if gens > 1:
         # KDE walks in launches of about one resident wave per slot (GEN_WAVES): all waves of a
         # launch start at the first node together and stay near each other in the node
@@ -374,8 +419,11 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
             xss.append(x.view(b1 - b0, n, -1) if n_out_cols else x)
         lp = torch.cat(lps) if plan.mode != MODE_SAMPLE else lps[0]
         x = torch.cat(xss) if n_out_cols else xss[0]
-    elif state is None:
+    elif state is None and run_if is None and out_x is None:
         lp, x = ops.walk(*args, plan.wbuf, plan_jit, precomp, precomp_q)
+    elif state is None:
+        lp, x = ops.walk_ex(*args, plan.wbuf, plan_jit, precomp, precomp_q, run_if=run_if,
+                            out_x=None if out_x is None else out_x.view(b * n, n_out_cols))
     else:
         lp, x = ops.walk_segment(*args, state, state_flags, step_begin, step_end, plan.wbuf)
     if plan.mode != MODE_SAMPLE:
@@ -468,13 +516,19 @@ class LikelihoodWeighting(_EngineBase):
         self.eps = float(eps)
         self.normalize = bool(normalize)
 
-    def _walk(self, vbn, query, n, *, clamp, shared_roots, kwargs, offset=0, noise=None):
+    def _walk(self, vbn, query, n, *, clamp, shared_roots, kwargs, offset=0, noise=None, run_if=None, out_x=None,
+              fixed_from=None):
+        """``fixed_from``: (fixed nodes, [B, fixed_ld] buffer) of an unclamped walk of the same
+        query (importance sampling's): with ``clamp`` and no do-values, this walk's buffer is
+        that one clamped as a whole (clamp_evidence, _core.py:112-114) -- two kernels instead of
+        two per evidence node plus the concatenation."""
         target, ev, do = self._query(query)
         b = infer_batch_size(ev, do)
         dev = _device_of(vbn)
         pk = packed_model(vbn, dev)
         model = pk.model
-        vals = _fixed_values(query, dev, clamp=clamp)
+        reuse = fixed_from is not None and clamp and not do and not _has_discrete(pk, list(ev))
+        vals = _fixed_values(query, dev, clamp=clamp and not reuse)
         _check_discrete(pk, vals, list(ev))
         keep = barren_pruned(model, [target] + list(ev)) if self.prune_barren else set(model.topo)
         key = ("weighted", target, tuple(sorted(ev)), tuple(sorted(do)), shared_roots, self.prune_barren)
@@ -483,12 +537,18 @@ class LikelihoodWeighting(_EngineBase):
                      logp=[x for x in model.topo if x in ev and x in keep], out_nodes=[target],
                      shared_roots=shared_roots, mode=MODE_WEIGHTED,
                      skip=[x for x in model.topo if x not in keep])
-        fx = _fixed_buffer(plan, vals, b, dev)
+        if reuse and tuple(fixed_from[0]) == tuple(plan.fixed_nodes):
+            fx = torch.nan_to_num(fixed_from[1], nan=0.0, posinf=1e6, neginf=-1e6).clamp_(min=-1e6, max=1e6)
+        else:
+            if reuse:                                  # other layout: clamp per node after all
+                vals = _fixed_values(query, dev, clamp=clamp)
+            fx = _fixed_buffer(plan, vals, b, dev)
+        self._last_fixed = (tuple(plan.fixed_nodes), fx)
         seed = kwargs.get("_seed_value")
         if seed is None:
             seed = self._seed(kwargs)
         log_w, xs = run_walk(pk, plan, fx, b, n, seed=seed, offset=offset, q_base=self.q_base, noise=noise,
-                             plan_jit=self.plan_jit)
+                             plan_jit=self.plan_jit, run_if=run_if, out_x=out_x)
         return log_w, xs
 
     def infer_posterior(self, vbn, query, **kwargs):
@@ -500,6 +560,15 @@ class LikelihoodWeighting(_EngineBase):
         w, _ = ops.normalize_weights(log_w, normalize, eps)
         return w, xs
 
+    def infer_into(self, vbn, query, n: int, *, seed: int, offset: int, run_if: torch.Tensor,
+                   w_out: torch.Tensor, x_out: torch.Tensor, noise=None, fixed_from=None) -> None:
+        """The whole LW call predicated on the device flag ``run_if``: pre-passes, walk and
+        normalisation write their weights / samples into ``w_out`` / ``x_out`` when it holds 1
+        and launch as no-ops otherwise (importance sampling's fallback without a host sync)."""
+        log_w, _ = self._walk(vbn, query, n, clamp=True, shared_roots=True, kwargs={"_seed_value": seed},
+                              offset=offset, noise=noise, run_if=run_if, out_x=x_out, fixed_from=fixed_from)
+        ops.normalize_weights_ex(log_w, self.normalize, self.eps, run_if=run_if, w_out=w_out)
+
 
 @register_inference("importance_sampling")
 class ImportanceSampling(LikelihoodWeighting):
@@ -509,7 +578,8 @@ class ImportanceSampling(LikelihoodWeighting):
         kwargs.pop("normalize", None)
         super().__init__(n_samples=n_samples, **kwargs)
         self.ess_threshold = 0.1
-        self._last_fallback = False
+        self._fallback_flag: Optional[torch.Tensor] = None    # device int32 [1] of the last call
+        self._fallback_bool: Optional[bool] = False
         self._last_ess: Optional[torch.Tensor] = None
         self._lw = LikelihoodWeighting(n_samples=self.n_samples, q_base=self.q_base,
                                        exact_f32=self.exact_f32, kde_valu=self.kde_valu,
@@ -520,23 +590,41 @@ class ImportanceSampling(LikelihoodWeighting):
         thr = max(1.0, self.ess_threshold * float(n))
         return (ess < thr).any()
 
+    @property
+    def _last_fallback(self) -> bool:
+        """Whether the last call fell back to likelihood weighting (the reference's attribute).
+        The decision stays on the device until this is read (one host sync, then cached)."""
+        if self._fallback_bool is None:
+            self._fallback_bool = bool(self._fallback_flag.item())
+        return self._fallback_bool
+
+    @_last_fallback.setter
+    def _last_fallback(self, value: bool) -> None:
+        self._fallback_flag, self._fallback_bool = None, bool(value)
+
+    def fallback_flag(self) -> Optional[torch.Tensor]:
+        """The last call's fallback decision as a device int32 [1] tensor (no host sync)."""
+        return self._fallback_flag
+
     def infer_posterior(self, vbn, query, **kwargs):
         n = int(kwargs.get("n_samples", self.n_samples))
         seed = self._seed(kwargs)
         log_w, xs = self._walk(vbn, query, n, clamp=False, shared_roots=False,
                                kwargs={**kwargs, "_seed_value": seed}, noise=kwargs.get("_noise"))
-        w, ess = ops.normalize_weights(log_w, True, 0.0)
+        # softmax + ESS, and the fallback decision (any ESS < threshold) on the device
+        thr = max(1.0, self.ess_threshold * float(n))
+        w, ess, flag = ops.normalize_weights_ex(log_w, True, 0.0, ess_thr=thr)
         self._last_ess = ess
-        flag = self.fallback_needed(ess, n)
         reduce = kwargs.get("_reduce_flag")          # multi-GPU: batch-global decision
         if reduce is not None:
-            flag = reduce(flag)
-        if bool(flag):                               # host sync, as the reference
-            self._last_fallback = True
-            self._lw.q_base = self.q_base
-            return self._lw.infer_posterior(vbn, query, n_samples=n, _seed_value=seed, _offset=1,
-                                            _noise=kwargs.get("_noise_fallback"))
-        self._last_fallback = False
+            flag = reduce(flag).to(device=w.device, dtype=torch.int32).reshape(1)
+        # importance_sampling.py:85-88: the likelihood-weighting re-draw replaces the outputs when
+        # the flag is set -- launched predicated on it and written into w / xs in place, so the
+        # host never waits for the decision (the reference syncs here)
+        self._lw.q_base = self.q_base
+        self._lw.infer_into(vbn, query, n, seed=seed, offset=1, run_if=flag, w_out=w, x_out=xs,
+                            noise=kwargs.get("_noise_fallback"), fixed_from=self._last_fixed)
+        self._fallback_flag, self._fallback_bool = flag, None
         return w, xs
 
 

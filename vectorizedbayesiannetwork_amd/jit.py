@@ -100,7 +100,8 @@ def plan_source(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=No
         *sweep,
         f'extern "C" __global__ void __launch_bounds__(WG_MAX_WAVES * WAVE) '
         f"__attribute__((amdgpu_waves_per_eu(VBN_WPE))) {KERNEL}(const vbn_walk_args A, "
-        f"const float* __restrict__ params) {{ vbn_walk_plan_body<{int(kind_set)}u>(A, params); }}",
+        f"const float* __restrict__ params) {{ if (A.run_if && *A.run_if == 0) return; "
+        f"vbn_walk_plan_body<{int(kind_set)}u>(A, params); }}",
         "",
     ])
 

@@ -52,6 +52,17 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
     2 = for every lean launch.  ``precomp`` / ``precomp_q``: the per-sample / per-query
     quantities of the table's VBN_F_PRECOMP steps ([S, stride] / [B, stride_q], the pre-pass
     walks' out_x; plan.precompute_plans)."""
+    return walk_ex(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
+                   fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed, offset,
+                   want_lp, kind_mask, wbuf, plan_jit, precomp, precomp_q)
+
+
+def walk_ex(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out, fixed_ld,
+            fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed, offset, want_lp,
+            kind_mask=63, wbuf=0, plan_jit=1, precomp=None, precomp_q=None, *, run_if=None, out_x=None):
+    """:func:`walk` as a plain launch, plus ``run_if`` (device int32 [1]: the launch does
+    nothing when it holds 0, vbn_walk_args.run_if) and ``out_x`` (write the samples into this
+    [B*S, n_out_cols] tensor; a predicated launch that does not run leaves it untouched)."""
     for name, t, rows, attr in (("precomp", precomp, n_samples, "_vbn_precomp_stride"),
                                 ("precomp_q", precomp_q, n_queries, "_vbn_precomp_q_stride")):
         need = getattr(steps, attr, None)
@@ -71,7 +82,7 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
     return _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots,
                         max_out, fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode,
                         q_base, seed, offset, want_lp, kind_mask, precomp, 4 if precomp is not None else 0,
-                        0, -1, wbuf, plan_jit, precomp_q)
+                        0, -1, wbuf, plan_jit, precomp_q, run_if=run_if, out_x=out_x)
 
 
 @torch.library.custom_op("vbn_hip::walk_segment", mutates_args=("state",))
@@ -112,7 +123,7 @@ def _check_wbuf(op: str, steps: Tensor, begin: int, end: int, wbuf: int) -> None
 def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                  fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
                  offset, want_lp, kind_mask, state, state_flags, step_begin, step_end, wbuf, plan_jit=0,
-                 precomp_q=None):
+                 precomp_q=None, run_if=None, out_x=None):
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::walk runs on the GPU only (no CPU fallback); "
@@ -144,7 +155,15 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
         if noise.numel() < need or noise_b not in (1, n_queries):
             raise ValueError(f"vbn_hip::walk: noise has {noise.numel()} values, needs {need}")
     lp = torch.empty(total if want_lp else 0, device=device, dtype=torch.float32)
-    x = torch.empty((total, n_out_cols) if n_out_cols > 0 else (0,), device=device, dtype=torch.float32)
+    if out_x is None:
+        x = torch.empty((total, n_out_cols) if n_out_cols > 0 else (0,), device=device, dtype=torch.float32)
+    else:
+        _check_dev("out_x", out_x, torch.float32, device)
+        if n_out_cols <= 0 or out_x.numel() != total * n_out_cols or not out_x.is_contiguous():
+            raise ValueError(f"vbn_hip::walk: out_x must be a contiguous [{total}, {n_out_cols}] float32 tensor")
+        x = out_x
+    if run_if is not None:
+        _check_dev("run_if", run_if, torch.int32, device)
     a = _lib.VbnWalkArgs()
     a.steps = steps.data_ptr() + step_begin * STEP_INTS * 4 if step_end > step_begin else None
     a.in_cols = _ptr(in_cols)
@@ -160,6 +179,7 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
     a.state = _ptr(state) if state_flags else None
     a.state_flags = int(state_flags)
     a.precomp_q = _ptr(precomp_q)
+    a.run_if = _ptr(run_if)
     a.n_slots = n_slots
     a.max_out = max_out
     a.fixed_ld = fixed_ld
@@ -328,18 +348,43 @@ def _gibbs_walk_fake(steps, in_cols, params, fixed, noise, state, n_queries, n_s
 
 @torch.library.custom_op("vbn_hip::normalize_weights", mutates_args=())
 def normalize_weights(log_w: Tensor, normalize: bool, eps: float) -> Tuple[Tensor, Tensor]:
+    w, ess, _ = normalize_weights_ex(log_w, normalize, eps)
+    return w, ess
+
+
+def normalize_weights_ex(log_w: Tensor, normalize: bool, eps: float, *, ess_thr: Optional[float] = None,
+                         run_if: Optional[Tensor] = None, w_out: Optional[Tensor] = None,
+                         ess_out: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
+    """The normalisation kernel (vbn_hip_normalize_weights_ex) as a plain launch: ``ess_thr``
+    returns a device int32 [1] flag, 1 when some query's ESS < ess_thr (importance_sampling.py
+    :85-86, decided without a host sync); ``run_if`` (device int32 [1]) predicates the launch;
+    ``w_out`` / ``ess_out``: write into these instead of fresh tensors (predicated launches
+    leave them untouched when *run_if == 0)."""
     if log_w.device.type != "cuda" or log_w.dtype != torch.float32 or log_w.dim() != 2:
         raise ValueError("vbn_hip::normalize_weights: log_w must be a float32 [B,S] GPU tensor")
     log_w = log_w.contiguous()
     b, s = log_w.shape
-    w = torch.empty_like(log_w)
-    ess = torch.empty(b, device=log_w.device, dtype=torch.float32)
+    w = torch.empty_like(log_w) if w_out is None else w_out
+    ess = torch.empty(b, device=log_w.device, dtype=torch.float32) if ess_out is None else ess_out
+    for name, t, shape in (("w_out", w_out, (b, s)), ("ess_out", ess_out, (b,))):
+        if t is not None and (t.dtype != torch.float32 or tuple(t.shape) != shape or not t.is_contiguous()
+                              or t.device != log_w.device):
+            raise ValueError(f"vbn_hip::normalize_weights: {name} must be a contiguous float32 {shape} tensor "
+                             "on log_w's device")
+    if run_if is not None:
+        _check_dev("run_if", run_if, torch.int32, log_w.device)
+    flag = None
+    if ess_thr is not None:
+        if not normalize:
+            raise ValueError("vbn_hip::normalize_weights: the ESS flag needs normalize=True")
+        flag = torch.zeros(1, device=log_w.device, dtype=torch.int32)
     lib = _lib.load()
     with torch.cuda.device(log_w.device):
-        _lib.check(lib.vbn_hip_normalize_weights(
+        _lib.check(lib.vbn_hip_normalize_weights_ex(
             _ptr(log_w), _ptr(w), _ptr(ess) if normalize else None, b, s, int(normalize), float(eps),
-            ctypes.c_void_p(_stream_handle(log_w.device))), "vbn_hip_normalize_weights")
-    return w, ess
+            _ptr(run_if), _ptr(flag), float(ess_thr or 0.0),
+            ctypes.c_void_p(_stream_handle(log_w.device))), "vbn_hip_normalize_weights_ex")
+    return w, ess, flag
 
 
 @normalize_weights.register_fake
@@ -449,8 +494,12 @@ def discrete_posterior(samples: Tensor, weights: Tensor, k: int) -> Tuple[Tensor
     if tuple(samples.shape[:2]) != tuple(weights.shape) or k <= 0:
         raise ValueError("vbn_hip::discrete_posterior: samples/weights shape mismatch or k <= 0")
     b, s = weights.shape
-    weights = weights.to(torch.float32).contiguous()
-    samples = samples.to(device=weights.device, dtype=torch.float32).contiguous()
+    # float32 / float64 elements as given (the reference's float() of each); other dtypes are
+    # converted to float32 (the engines' outputs are float32)
+    keep = (torch.float32, torch.float64)
+    weights = (weights if weights.dtype in keep else weights.to(torch.float32)).contiguous()
+    samples = samples.to(device=weights.device)
+    samples = (samples if samples.dtype in keep else samples.to(torch.float32)).contiguous()
     stride = samples.shape[2] if samples.dim() == 3 else 1
     probs = torch.empty(b, k, device=weights.device, dtype=torch.float64)
     bad = torch.empty(b, device=weights.device, dtype=torch.int32)
@@ -460,9 +509,10 @@ def discrete_posterior(samples: Tensor, weights: Tensor, k: int) -> Tuple[Tensor
         return probs, bad
     lib = _lib.load()
     with torch.cuda.device(weights.device):
-        _lib.check(lib.vbn_hip_discrete_posterior(
-            _ptr(samples), stride, _ptr(weights), _ptr(probs), _ptr(bad), b, s, int(k),
-            ctypes.c_void_p(_stream_handle(weights.device))), "vbn_hip_discrete_posterior")
+        _lib.check(lib.vbn_hip_discrete_posterior_typed(
+            _ptr(samples), int(samples.dtype == torch.float64), stride, _ptr(weights),
+            int(weights.dtype == torch.float64), _ptr(probs), _ptr(bad), b, s, int(k),
+            ctypes.c_void_p(_stream_handle(weights.device))), "vbn_hip_discrete_posterior_typed")
     return probs, bad
 
 
