@@ -48,21 +48,66 @@ def test_query_ops_equal_engines(cfg_name, method):
     elif method == "ancestral":
         ref = (SAMPLING_REGISTRY[method](n_samples=s).sample(vbn, q, s, seed=seed),)
         got = (ops.ancestral(packed["plan"], packed["params"], fixed, s, seed),)
-    else:
-        lw = method == "likelihood_weighting"
-        eng = INFERENCE_REGISTRY[method](n_samples=s)
-        ref = eng.infer_posterior(vbn, q, seed=seed)
-        w, x, ess, flag = ops.is_lw(packed["plan"], packed["params"], fixed, s, seed, lw_mode=lw)
-        if not lw:
-            assert bool(flag) == eng._last_fallback
-            if eng._last_fallback:
-                pytest.skip("the IS -> LW fallback fired (its LW walk is another signature)")
-            assert torch.equal(ess, eng._last_ess)
+    elif method == "likelihood_weighting":
+        ref = INFERENCE_REGISTRY[method](n_samples=s).infer_posterior(vbn, q, seed=seed)
+        w, x, ess, flag = ops.is_lw(packed["plan"], packed["params"], fixed, s, seed, lw_mode=True)
         got = (w, x)
+    else:
+        _check_is_op(vbn, sig, packed, q, ev, b, s, seed)
+        return
+    _equal(got, ref)
+
+
+def _equal(got, ref):
     torch.cuda.synchronize()
     for g, r in zip(got, ref):
         assert g.shape == r.shape, (g.shape, r.shape)
         assert torch.equal(torch.nan_to_num(g, 7.0, 8.0, 9.0), torch.nan_to_num(r, 7.0, 8.0, 9.0))
+
+
+def _check_is_op(vbn, sig, packed, q, ev, b, s, seed, expect_fallback=None):
+    """vbn_hip::is_lw against the engine: the op's IS weights / samples / ESS equal the engine's
+    walk before its fallback decision, its flag equals the engine's decision, and when the
+    fallback fired, the caller's re-draw -- is_lw(lw_mode=True) on the likelihood-weighting
+    signature with the engine's RNG offset 1 and clamped evidence -- equals the engine's final
+    output (importance_sampling.py:82-88)."""
+    from vectorizedbayesiannetwork_amd.registry import INFERENCE_REGISTRY
+    ops = torch.ops.vbn_hip
+    eng = INFERENCE_REGISTRY["importance_sampling"](n_samples=s)
+    ref = eng.infer_posterior(vbn, q, seed=seed)
+    w, x, ess, flag = ops.is_lw(packed["plan"], packed["params"], _fixed(packed, ev, b), s, seed)
+    assert bool(flag) == eng._last_fallback
+    if expect_fallback is not None:
+        assert eng._last_fallback == expect_fallback
+    assert torch.equal(torch.nan_to_num(ess, 7.0), torch.nan_to_num(eng._last_ess, 7.0))
+    # the engine's IS walk and normalisation before the decision
+    log_w, px = eng._walk(vbn, q, s, clamp=False, shared_roots=False, kwargs={"_seed_value": seed})
+    pw, _ = ops.normalize_weights(log_w, True, 0.0)
+    _equal((w, x), (pw, px))
+    if not eng._last_fallback:
+        _equal((w, x), ref)
+        return
+    pl = vbn.pack_query(sig, "likelihood_weighting", n_samples=s)
+    lw_w, lw_x, _, lw_flag = ops.is_lw(pl["plan"], pl["params"], _fixed(pl, ev, b, clamp=True), s, seed, 1,
+                                       lw_mode=True)
+    assert not bool(lw_flag)
+    _equal((lw_w, lw_x), ref)
+
+
+def test_query_op_is_fallback_redraw():
+    """The IS -> LW fallback through the query ops: off-manifold evidence in one query (an
+    evidence node with latent parents, so its log-weight varies over the particles) collapses
+    that query's ESS and fires the batch-global fallback."""
+    from vectorizedbayesiannetwork_amd.engines import Query
+    model, vbn, target, ev = synthetic_workload("cfg2", B, "cuda")
+    par = model.parents
+    k0 = next(k for k in sorted(ev) if par[k] and not any(p in ev for p in par[k]))
+    ev = {k: v.clone() for k, v in ev.items()}
+    ev[k0][B - 1, 0] = 50.0
+    sig = {"target": target, "evidence": list(ev)}
+    packed = vbn.pack_query(sig, "importance_sampling", n_samples=S)
+    q = Query(target, {k: v.cuda() for k, v in ev.items()})
+    _check_is_op(vbn, sig, packed, q, ev, B, S, 8181, expect_fallback=True)
 
 
 def test_pack_plan_round_trip_and_errors():

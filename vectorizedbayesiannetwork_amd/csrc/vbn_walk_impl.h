@@ -1264,14 +1264,14 @@ __device__ __forceinline__ float kde_qy(const float* __restrict__ pty, float x0,
 // The kernel weight of particle n and stored point m is exp(-|x_n - y_m|^2 / (2 s^2)) =
 // exp2(-|x'_n - y'_m|^2) with x' = c x, y' = c y, c = sqrt(log2(e) / 2) / s, and
 //   -|x' - y'|^2 = sum_k (2 x'_k) y'_k - |y'|^2 - |x'|^2,
-// a contraction over K <= 3 features, computed on bf16 MFMAs from exact three-way splits
-// (kde_bf16_sums below) for the inverse-CDF chunk sums and the log-density sums alike.
-// Padding points have |y'|^2 = 1e30 -> weight 0.  The wave's 64 particles are 4 tiles of 16
-// (tile t = particles 16t .. 16t+15); D layout: lane l holds points 4(l>>4) .. +3 of the block
-// for particle 16t + (l&15).  Bound: v_exp_f32 issue (one exp per pair).  The inverse-CDF scan
+// a contraction over K <= 4 features, computed on bf16 MFMAs from exact three-way splits
+// (kde_b32_sums below) for the inverse-CDF chunk sums and the log-density sums alike.
+// Padding points have |y'|^2 = 1e30 -> weight 0.  The wave's 64 particles are 2 tiles of 32
+// (tile t = particles 32t .. 32t+31); D layout: lane l holds points 8j + 4(l>>5) + i (j, i < 4)
+// of the block for particle 32t + (l&31).  Bound: v_exp_f32 issue (one exp per pair).  The inverse-CDF scan
 // recomputes its chunk's weights with kde_arg_rec, the float32 chain of the same contraction
 // (equal to the MFMA sums to f32 rounding; a crossing past the chunk end is clamped, kde_scan).
-// the lane's own particle: x'_k and -|x'|^2 exactly as kde_bf16_ops computes them
+// the lane's own particle: x'_k and -|x'|^2 exactly as kde_b32_ops computes them
 __device__ __forceinline__ float kde_own(const Lane& L, const int (&slots)[4], const float (&scl)[4], int nf,
                                          float (&xv)[4]) {
   float sq = 0.f;
@@ -1297,22 +1297,12 @@ __device__ __forceinline__ float kde_arg_rec(const float4 r, float xb0, float xb
   return zc ? fmaf(1.f, negsq, d) : d;
 }
 
-// Blocks per chunk: a multiple of 4 (the host pads the pack to KDE_CHUNKS * kde_cb(M) blocks).
+// 16-point blocks per chunk: a multiple of 4, so a chunk is a whole number of the MFMA pass's
+// KDE_PF = 2 blocks of 32 points (the host pads the packs to KDE_CHUNKS * kde_cb(M) 16-point
+// blocks)
 __device__ __forceinline__ int kde_cb(int M) {
   const int nblk = (M + 15) >> 4;
   return (((nblk + KDE_CHUNKS - 1) / KDE_CHUNKS) + 3) & ~3;
-}
-
-// Sum of the lane's 4 tile partials across the 4 lane groups: lane l receives the total of
-// particle l (tile l>>4, column l&15).  Three cross-lane moves.
-__device__ __forceinline__ float kde_reduce_tiles(const float (&s)[4], int lane) {
-  const int h = lane >> 5, b = (lane >> 4) & 1;
-  float k0 = h ? s[2] : s[0], k1 = h ? s[3] : s[1];
-  const float o0 = h ? s[0] : s[2], o1 = h ? s[1] : s[3];
-  k0 += __shfl_xor(o0, 32);
-  k1 += __shfl_xor(o1, 32);
-  const float k = b ? k1 : k0, o = b ? k0 : k1;
-  return k + __shfl_xor(o, 16);
 }
 
 // Point operands are prefetched a whole trip ahead, across chunk boundaries: the packs of a
@@ -1327,23 +1317,27 @@ __device__ __forceinline__ float kde_reduce_tiles(const float (&s)[4], int lane)
 #define KDE_BLK(x) (x)
 #endif
 
-// Pass-1 sums on v_mfma_f32_16x16x32_bf16 ("bf16x3"): rows = 16 points, columns = the 16
-// particles of tile t, K = 32 slots.  Every f32 operand is split into three bf16 whose sum is
-// it exactly (hi = bf16(v), mid = bf16(v - hi), lo = the 8-bit rest); per feature the six
+// Pass-1 sums on v_mfma_f32_32x32x16_bf16 ("bf16x3", round 5): rows = 32 points, columns =
+// the 32 particles of tile t (particles 32 t .. 32 t + 31), K = 16 slots (one MFMA, nf = 1) or
+// 32 (two chained MFMAs, nf = 2..4).  Every f32 operand is split into three bf16 whose sum is
+// it exactly (hi = bf16(v), mid = bf16(v - hi), lo = the 8-bit rest); per feature f the six
 // products u_h y_h, u_h y_m, u_m y_h, u_h y_l, u_l y_h, u_m y_m (u = 2x' on the B side, y' on
-// the A side; the omitted terms are < 2^-25 of u y) are exact in f32, |y'|^2's three parts meet
-// -1 and 1.0 meets -|x'|^2's three parts, so the MFMA's f32 sum from C = 0 is the 16x16x4
-// form's contraction to f32 rounding (tests/test_plan.py).  One bf16 MFMA per tile and 16
-// points -- 16 cycles of the matrix pipe per 256 pairs, which the 16 exps per lane it feeds
-// hide -- against the f32 16x16x4 MFMA's 32 cycles, during which VALU issue also stalls
-// (profiles/microbench/coissue_sgb_r03.json).  A = host pack (plan.py _kde_pack_bf16)
-// [block][quarter][16][8]: lane l loads point l & 15's slots 8 (l >> 4) .. +7 (16 B, 1 KiB per
-// wave and block); B = kde_bf16_ops, 4 VGPRs per tile; D: the 16x16x4 form's layout, so
-// kde_reduce_tiles finishes the per-particle sums.
+// the A side, slots 6f .. 6f+5; the omitted ones are < 2^-25 of u y) are exact in f32,
+// |y'|^2's three parts (slots 6nf .. +2) meet -1 and 1.0 (6nf+3 .. +5) meets -|x'|^2's three
+// parts, so the MFMA's f32 sum from C = 0 is the contraction -|x' - y'|^2 to f32 rounding
+// (tests/test_plan.py).  Against round 4's v_mfma_f32_16x16x32_bf16 tiles the wave issues a
+// quarter of the MFMAs per pair (one 32x32x16 per 1,024 pairs instead of four 16x16x32, each
+// holding the SIMD's vector issue for 8 cycles) and reads 32 instead of 64 bytes per point
+// for nf = 1; the 16 exps per lane and MFMA are summed with plain f32 adds (4 accumulators
+// per tile; packed f32 adds beside MFMAs cost extra issue cycles, MI355X_MICROARCH.md).
+// A = host pack (plan.py _kde_pack_b32) [block of 32][K group g][64 lanes][8]: lane l loads
+// point l & 31's slots 16 g + 8 (l >> 5) .. +7 (16 B, 1 KiB per wave, block and K group);
+// B = kde_b32_ops; D: lane l holds rows 8 j + 4 (l >> 5) + i (j, i < 4) of column l & 31.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-struct KdeBOps {
-  bf16x8 b[4];      // tile t: particle 16 t + (lane & 15), slots 8 (lane >> 4) .. +7
+template <int KG>
+struct KdeB32 {
+  bf16x8 b[2][KG];  // tile t: particle 32 t + (lane & 31), slots 16 g + 8 (lane >> 5) .. +7
 };
 
 __device__ __forceinline__ void bf16_split3(float v, __bf16 (&p)[3]) {
@@ -1353,73 +1347,146 @@ __device__ __forceinline__ void bf16_split3(float v, __bf16 (&p)[3]) {
   p[2] = (__bf16)(r1 - (float)p[1]);
 }
 
-// slot k (0..31) of the B operand: feature splits sp (_BF16_B pattern), -1 x 3, split of -|x'|^2
-__device__ __forceinline__ __bf16 kde_bslot(int k, int nf, const __bf16 (&sp)[3][3], const __bf16 (&sx)[3]) {
+// slot k of the B operand: feature splits sp (_BF16_B pattern), -1 x 3, split of -|x'|^2, 0
+__device__ __forceinline__ __bf16 kde_bslot(int k, int nf, const __bf16 (&sp)[4][3], const __bf16 (&sx)[3]) {
   constexpr int pat[6] = {0, 0, 1, 0, 2, 1};
-  if (k < 18) return (k / 6) < nf ? sp[k / 6][pat[k % 6]] : (__bf16)0.f;
-  if (k < 21) return (__bf16)-1.f;
-  if (k < 24) return sx[k - 21];
+  const int f = k / 6;
+  if (f < nf) return sp[f][pat[k - 6 * f]];
+  const int r = k - 6 * nf;
+  if (r < 3) return (__bf16)-1.f;
+  if (r < 6) return sx[r - 3];
   return (__bf16)0.f;
 }
 
-// -|x'|^2 exactly as kde_own accumulates it
-__device__ __forceinline__ void kde_bf16_ops(const Lane& L, const int (&slots)[4], const float (&scl)[4], int nf,
-                                             KdeBOps& o) {
-  const int g = L.lane >> 4, n = L.lane & 15;
+// the lane's particle side of tile t; -|x'|^2 exactly as kde_own accumulates it
+template <int KG>
+__device__ __forceinline__ void kde_b32_ops(const Lane& L, const int (&slots)[4], const float (&scl)[4], int nf,
+                                            KdeB32<KG>& o) {
+  const int h = L.lane >> 5, n = L.lane & 31;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < 2; ++t) {
     float sq = 0.f;
-    __bf16 sp[3][3], sx[3];
+    __bf16 sp[4][3], sx[3];
 #pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      const float v = f < nf ? scl[f] * L.vals[slots[f] * WAVE + 16 * t + n] : 0.f;
+    for (int f = 0; f < 4; ++f) {
+      const float v = f < nf ? scl[f] * L.vals[slots[f] * WAVE + 32 * t + n] : 0.f;
       if (f < nf) sq = fmaf(v, v, sq);
       bf16_split3(2.f * v, sp[f]);
     }
     bf16_split3(-sq, sx);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const __bf16 v0 = kde_bslot(j, nf, sp, sx), v1 = kde_bslot(8 + j, nf, sp, sx);
-      const __bf16 v2 = kde_bslot(16 + j, nf, sp, sx), v3 = kde_bslot(24 + j, nf, sp, sx);
-      o.b[t][j] = g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
-    }
-  }
-}
-
-// per-lane tile partial sums of exp2(arg) over 16-point blocks [b0, b1) of the bf16x3 pack
-// (pa = pack + lane), b1 - b0 a multiple of 4; nx holds blocks b0 .. b0+3 on entry and
-// b1 .. b1+3 on return (kde_bf16_prefetch4): each trip loads the next trip's four operands
-// before its 16 MFMAs and 64 exps.
-__device__ __forceinline__ void kde_bf16_prefetch4(const bf16x8* __restrict__ pa, int b0, int blast, bf16x8 (&nx)[4]) {
+    for (int g = 0; g < KG; ++g) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) nx[u] = pa[KDE_BLK(min(b0 + u, blast)) * 64];
-}
-
-__device__ __forceinline__ void kde_bf16_sums(const bf16x8* __restrict__ pa, int b0, int b1, int blast,
-                                              const KdeBOps& o, float (&s)[4], bf16x8 (&nx)[4]) {
-  f32x2 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = f32x2{0.f, 0.f};
-  for (int b = b0; b < b1; b += 4) {
-    const bf16x8 a[4] = {nx[0], nx[1], nx[2], nx[3]};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) nx[u] = pa[KDE_BLK(min(b + 4 + u, blast)) * 64];   // next trip's operands
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      f32x4 d[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        d[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u], o.b[t], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const f32x2 e01 = f32x2{__builtin_amdgcn_exp2f(d[t][0]), __builtin_amdgcn_exp2f(d[t][1])};
-        const f32x2 e23 = f32x2{__builtin_amdgcn_exp2f(d[t][2]), __builtin_amdgcn_exp2f(d[t][3])};
-        acc[t] += e01 + e23;
+      for (int j = 0; j < 8; ++j) {
+        const __bf16 v0 = kde_bslot(16 * g + j, nf, sp, sx), v1 = kde_bslot(16 * g + 8 + j, nf, sp, sx);
+        o.b[t][g][j] = h ? v1 : v0;
       }
     }
   }
+}
+
+// Sum over a chunk's 32-point blocks of the lane's tile partials: lane l receives the total of
+// particle l (tile l >> 5, column l & 31): one cross-lane move.
+__device__ __forceinline__ float kde_reduce_tiles(const float (&s)[2], int lane) {
+  const int h = lane >> 5;
+  const float k = h ? s[1] : s[0], o = h ? s[0] : s[1];
+  return k + __shfl_xor(o, 32);
+}
+
+// one 32-point block: KG chained MFMAs per tile, 16 exps per tile summed into 4 accumulators
+template <int KG>
+__device__ __forceinline__ void kde_b32_block(const bf16x8 (&a)[KG], const KdeB32<KG>& o, float (&acc)[2][4]) {
+  f32x16 d[2];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) s[t] += acc[t].x + acc[t].y;
+  for (int t = 0; t < 2; ++t) {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[i] = 0.f;
+    d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], o.b[t][0], z, 0, 0, 0);
+    if constexpr (KG == 2) d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], o.b[t][1], d[t], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i & 3] += __builtin_amdgcn_exp2f(d[t][i]);
+  }
+}
+
+// block b's operands (clamped to the pack's last block; pa = pack + lane)
+template <int KG>
+__device__ __forceinline__ void kde_b32_load(const bf16x8* __restrict__ pa, int b, int blast, bf16x8 (&a)[KG]) {
+  const int bb = KDE_BLK(min(b, blast));
+#pragma unroll
+  for (int g = 0; g < KG; ++g) a[g] = pa[(bb * KG + g) * 64];
+}
+
+// Operands of the next KDE_PF blocks in flight (a ring of KDE_PF operand sets): block b's set
+// is used, then reloaded with block b + KDE_PF, so every load has KDE_PF - 1 blocks of exps in
+// front of its use.  The ring continues across calls (chunks) without a reload.
+#define KDE_PF 2             // kde_cb keeps every chunk a multiple of 2 blocks of 32 points
+template <int KG>
+struct KdeTrip {
+  bf16x8 x[KDE_PF][KG];
+};
+
+template <int KG>
+__device__ __forceinline__ void kde_b32_prefetch(const bf16x8* __restrict__ pa, int b0, int blast, KdeTrip<KG>& q) {
+#pragma unroll
+  for (int u = 0; u < KDE_PF; ++u) kde_b32_load<KG>(pa, b0 + u, blast, q.x[u]);
+}
+
+// per-lane tile partial sums of exp2(arg) over 32-point blocks [b0, b1), b1 - b0 a multiple of
+// KDE_PF (kde_cb)
+template <int KG>
+__device__ __forceinline__ void kde_b32_sums(const bf16x8* __restrict__ pa, int b0, int b1, int blast,
+                                             const KdeB32<KG>& o, float (&s)[2], KdeTrip<KG>& q) {
+  float acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[t][i] = 0.f;
+  for (int b = b0; b < b1; b += KDE_PF) {
+#pragma unroll
+    for (int u = 0; u < KDE_PF; ++u) {
+      kde_b32_block<KG>(q.x[u], o, acc);
+      kde_b32_load<KG>(pa, b + KDE_PF + u, blast, q.x[u]);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) s[t] += (acc[t][0] + acc[t][1]) + (acc[t][2] + acc[t][3]);
+}
+
+// Pass 1 of a node with nf features over its KDE_CHUNKS chunks: chunk sums -> scr[chunk][lane]
+template <int KG>
+__device__ __forceinline__ double kde_pass1(const bf16x8* __restrict__ pa, int cb32, const Lane& L,
+                                            const int (&slots)[4], const float (&scl)[4], int nf) {
+  KdeB32<KG> o;
+  kde_b32_ops<KG>(L, slots, scl, nf, o);
+  const int blast = KDE_CHUNKS * cb32 - 1;
+  KdeTrip<KG> q;
+  kde_b32_prefetch<KG>(pa, 0, blast, q);
+  double tot = 0.0;
+  for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+    float s[2] = {0.f, 0.f};
+    kde_b32_sums<KG>(pa, ch * cb32, ch * cb32 + cb32, blast, o, s, q);
+    const float cs = kde_reduce_tiles(s, L.lane);
+    L.scr[ch * WAVE + L.lane] = cs;
+    tot += (double)cs;
+  }
+  return tot;
+}
+
+// Sum over all nb32 blocks of a log-density pack (kde_logp_mfma)
+template <int KG>
+__device__ __forceinline__ float kde_sum_all(const bf16x8* __restrict__ pa, int nb32, const Lane& L,
+                                             const int (&slots)[4], const float (&scl)[4], int nf) {
+  KdeB32<KG> o;
+  kde_b32_ops<KG>(L, slots, scl, nf, o);
+  KdeTrip<KG> q;
+  kde_b32_prefetch<KG>(pa, 0, nb32 - 1, q);
+  float s[2] = {0.f, 0.f};
+  kde_b32_sums<KG>(pa, 0, nb32, nb32 - 1, o, s, q);
+  return kde_reduce_tiles(s, L.lane);
 }
 
 // Inverse-CDF scan of one chunk [j0, j1) (pass 2).  A lane whose threshold lies in the upper
@@ -1500,18 +1567,7 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
 #endif
   {
     const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
-    KdeBOps o;
-    kde_bf16_ops(L, slots, scl, nf, o);
-    const int blast = KDE_CHUNKS * cb - 1;
-    bf16x8 nx[4];
-    kde_bf16_prefetch4(pa, 0, blast, nx);
-    for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-      float s[4] = {0.f, 0.f, 0.f, 0.f};
-      kde_bf16_sums(pa, ch * cb, ch * cb + cb, blast, o, s, nx);
-      const float cs = kde_reduce_tiles(s, lane);
-      L.scr[ch * WAVE + lane] = cs;
-      tot += (double)cs;
-    }
+    tot = nf == 1 ? kde_pass1<1>(pa, cb >> 1, L, slots, scl, nf) : kde_pass1<2>(pa, cb >> 1, L, slots, scl, nf);
   }
   const int nfr = nf;                                 // replica form of the pass-1 elements
   const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
@@ -1578,30 +1634,18 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
 __device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L, bool root, float c_p,
                                               float c_y, float cy, float log_n, float& lp) {
   const int M = st.k, dp = st.aux0, D = st.out_dim, lane = L.lane;
-  const int nb = (((M + 15) >> 4) + 3) & ~3;
+  const int nb32 = (KDE_CHUNKS * kde_cb(M)) >> 1;
   int slots[4] = {0, 0, 0, 0};
   float scl[4] = {c_p, c_p, c_p, c_p};
   for (int f = 0; f < dp; ++f) slots[f] = L.ic[st.in_off + f];
   for (int d = 0; d < D; ++d) { slots[dp + d] = st.out_col + d; scl[dp + d] = c_y; }
-  float sy4[4] = {0.f, 0.f, 0.f, 0.f}, sp4[4] = {0.f, 0.f, 0.f, 0.f};
-  {
-    const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[2]) + lane;
-    KdeBOps oy;
-    kde_bf16_ops(L, slots, scl, dp + D, oy);
-    bf16x8 nx[4];
-    kde_bf16_prefetch4(pa, 0, nb - 1, nx);
-    kde_bf16_sums(pa, 0, nb, nb - 1, oy, sy4, nx);
-  }
-  const float sy = kde_reduce_tiles(sy4, lane);
+  const int ny = dp + D;
+  const bf16x8* __restrict__ pay = reinterpret_cast<const bf16x8*>(L.P + st.reserved[2]) + lane;
+  const float sy = ny == 1 ? kde_sum_all<1>(pay, nb32, L, slots, scl, ny) : kde_sum_all<2>(pay, nb32, L, slots, scl, ny);
   float sp = 1.f;
   if (!root) {
     const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
-    KdeBOps op;
-    kde_bf16_ops(L, slots, scl, dp, op);
-    bf16x8 nx[4];
-    kde_bf16_prefetch4(pa, 0, nb - 1, nx);
-    kde_bf16_sums(pa, 0, nb, nb - 1, op, sp4, nx);
-    sp = kde_reduce_tiles(sp4, lane);
+    sp = dp == 1 ? kde_sum_all<1>(pa, nb32, L, slots, scl, dp) : kde_sum_all<2>(pa, nb32, L, slots, scl, dp);
   }
   wave_sync();
   if (!(sy > 0.f) || !(sp > 0.f)) return false;

@@ -87,7 +87,8 @@ _KDE_C = math.sqrt(0.5 * math.log2(math.e))      # exp(-d^2 / 2) = exp2(-(c d)^2
 
 
 def _kde_cb(m: int) -> int:
-    """16-point blocks per inverse-CDF chunk (a multiple of 4; csrc kde_cb)."""
+    """16-point blocks per inverse-CDF chunk (a multiple of 4: whole pairs of the 32-point
+    blocks of the MFMA pass; csrc kde_cb)."""
     nblk = (m + 15) // 16
     return ((nblk + KDE_CHUNKS - 1) // KDE_CHUNKS + 3) & ~3
 
@@ -145,36 +146,36 @@ def _bf16_split3(v: np.ndarray):
 # six products are u_h y_h, u_h y_m, u_m y_h, u_h y_l, u_l y_h, u_m y_m (csrc kde_bf16_sums)
 _BF16_A = (0, 1, 0, 2, 0, 1)
 _BF16_B = (0, 0, 1, 0, 2, 1)
-KDE_BF16_K = 32                       # slots per point (v_mfma_f32_16x16x32_bf16)
 
 
-def _kde_pack_bf16(y: np.ndarray) -> np.ndarray:
-    """Point pack of the bf16x3 pass (csrc kde_bf16_sums): A operand of
-    v_mfma_f32_16x16x32_bf16, rows = 16 points per block, K = 32 slots per point: feature f at
-    slots 6f .. 6f+5 (_BF16_A of its hi / mid / lo split; zero for f >= nf), |y'|^2's hi / mid /
-    lo at 18-20 (B side -1), 1.0 at 21-23 (B side: the split of -|x'|^2), 24-31 zero.  Layout
-    [block][quarter][16 points][8 slots] bf16 (lane l loads point l & 15's slots 8 (l >> 4) ..
-    +7 as one 16-byte load); the same points, |y'|^2, padding (|y'|^2 = 1e30) and blocks as
-    _kde_pack (KDE_CHUNKS * cb blocks of 16), so chunk boundaries coincide."""
+def _kde_pack_b32(y: np.ndarray) -> np.ndarray:
+    """Point pack of the bf16x3 pass (csrc kde_b32_sums): A operand of
+    v_mfma_f32_32x32x16_bf16, rows = 32 points per block, K = 16 slots per point for one feature
+    and 32 (two chained MFMAs) for 2-4: feature f at slots 6f .. 6f+5 (_BF16_A of its hi / mid /
+    lo split), |y'|^2's hi / mid / lo at 6nf .. 6nf+2 (B side -1), 1.0 at 6nf+3 .. 6nf+5 (B
+    side: the split of -|x'|^2), zero after.  Layout [block][K group g][half h][32 points][8
+    slots] bf16: lane l = 32 h + n loads point n's slots 16 g + 8 h .. +7 as one 16-byte load;
+    the points padded to KDE_CHUNKS * _kde_cb(M) * 16 (|y'|^2 = 1e30: weight 0), so a chunk is
+    _kde_cb(M) / 2 blocks and its boundaries are the record scan's."""
     y = y.reshape(y.shape[0], -1).astype(np.float32)
     m, nf = y.shape
-    if not 1 <= nf <= 3:
-        raise ValueError("the bf16x3 KDE pack is for 1-3 features")
-    nblk = KDE_CHUNKS * _kde_cb(m)
-    rows = nblk * 16
+    if not 1 <= nf <= 4:
+        raise ValueError("the bf16x3 KDE pack is for 1-4 features")
+    kg = 1 if nf == 1 else 2
+    rows = KDE_CHUNKS * _kde_cb(m) * 16
     feats = np.zeros((rows, nf), np.float32)
     feats[:m] = y
     sq = np.full(rows, 1e30, np.float32)
     sq[:m] = (y.astype(np.float64) ** 2).sum(axis=1).astype(np.float32)
-    slots = np.zeros((rows, KDE_BF16_K), np.uint16)
+    slots = np.zeros((rows, 16 * kg), np.uint16)
     for f in range(nf):
         sp = _bf16_split3(feats[:, f])
         for j in range(6):
             slots[:, 6 * f + j] = sp[_BF16_A[j]]
     for j, h in enumerate(_bf16_split3(sq)):
-        slots[:, 18 + j] = h
-    slots[:, 21:24] = 0x3F80                                  # bf16 1.0
-    a = slots.reshape(nblk, 16, 4, 8).transpose(0, 2, 1, 3)   # [blk][quarter][16][8]
+        slots[:, 6 * nf + j] = h
+    slots[:, 6 * nf + 3:6 * nf + 6] = 0x3F80                   # bf16 1.0
+    a = slots.reshape(rows // 32, 32, kg, 2, 8).transpose(0, 2, 3, 1, 4)   # [blk][g][h][32][8]
     return np.ascontiguousarray(a).reshape(-1).view(np.float32)
 
 
@@ -385,15 +386,15 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
         c_y = np.float32(_KDE_C / s_y)
         offs["tail"] = blob.add(np.array([1.0 / np.float32(s_p), 1.0 / np.float32(s_y),
                                           noise_scale, cy, math.log(float(m)), c_p, c_y, 0], np.float32))
-        # MFMA packs (csrc/vbn_walk_impl.h, kde_bf16_sums): bf16x3 point slots, [block][quarter][16][8]
+        # MFMA packs (csrc/vbn_walk_impl.h, kde_b32_sums): bf16x3 point slots, [block][g][h][32][8]
         if 1 <= dp <= 3:
-            offs["kq"] = blob.add(_kde_pack_bf16(_np(pts_p) * c_p))
+            offs["kq"] = blob.add(_kde_pack_b32(_np(pts_p) * c_p))
             offs["kr"] = blob.add(_kde_pack([_np(pts_p) * c_p], records=True))
             offs["kv"] = blob.add(_kde_pack_valu(_np(pts_p) * c_p))
-        if dp + D <= 3:
+        if dp + D <= 4:
             feats = np.concatenate(([_np(pts_p).reshape(m, -1) * c_p] if dp else [])
                                    + [_np(pts_y).reshape(m, -1) * c_y], axis=1)
-            offs["kqy"] = blob.add(_kde_pack_bf16(feats))
+            offs["kqy"] = blob.add(_kde_pack_b32(feats))
         stride = dp + D
         stride += (-stride) % 2 if stride > 1 else 0
         recs = np.zeros((m, stride), np.float32)
