@@ -11,6 +11,8 @@
 //               factored out), 2 tiles of 32 particles, 16 exps per MFMA, plain f32 adds
 //   p32       : s32 with f32x2 adds
 //   s32k32    : K = 32 (3 features) as two chained 32x32x16 MFMAs per tile, plain adds
+//   w1s / w1p : the walk's round-5 form (a ring of 2 operand blocks), K = 16, plain / f32x2 adds
+//   w2s / w2p : the same with K = 32 (two chained MFMAs per tile and block), M / 2 points
 // Prints ms per launch and pair rate against the v_exp_f32 issue peak (8 cycles per wave64
 // instruction and SIMD, 1024 SIMDs, 2.4 GHz = 19.66 T/s).
 #include <hip/hip_runtime.h>
@@ -293,6 +295,73 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
   out[blockIdx.x * 64 + lane] = (float)tot;
 }
 
+// ---- w<KG><s|p>: the walk's round-5 form (csrc kde_b32_sums): a ring of 2 operand blocks,
+// KG chained 32x32x16 MFMAs per tile and block, plain (s) or f32x2 (p) adds -------------------
+template <int KG, bool PK>
+__device__ __forceinline__ void wblock(const bf16x8 (&a)[KG], const bf16x8 (&ob)[2][KG], float (&acc)[2][4],
+                                       f32x2 (&pacc)[2][2]) {
+  f32x16 d[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[i] = 0.f;
+    d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], ob[t][0], z, 0, 0, 0);
+    if constexpr (KG == 2) d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], ob[t][1], d[t], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if constexpr (PK) {
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        pacc[t][0] += f32x2{__builtin_amdgcn_exp2f(d[t][i]), __builtin_amdgcn_exp2f(d[t][i + 1])};
+        pacc[t][1] += f32x2{__builtin_amdgcn_exp2f(d[t][i + 2]), __builtin_amdgcn_exp2f(d[t][i + 3])};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i & 3] += __builtin_amdgcn_exp2f(d[t][i]);
+    }
+  }
+}
+
+template <int KG, bool PK>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_walk(const bf16x8* __restrict__ pack, float* out, float seed) {
+  const int lane = threadIdx.x;
+  bf16x8 ob[2][KG];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int g = 0; g < KG; ++g) ob[t][g] = bop(lane, t + 2 * g, seed);
+  const bf16x8* __restrict__ pa = pack + lane;
+  const int nb = KG == 1 ? NB32 : NB32 / 2;             // same bytes read for both K sizes
+  const int cb = nb / CHUNKS, blast = nb - 1;
+  bf16x8 x[2][KG];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int g = 0; g < KG; ++g) x[u][g] = pa[(min(u, blast) * KG + g) * 64];
+  double tot = 0.0;
+  for (int ch = 0; ch < CHUNKS; ++ch) {
+    float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x2 pacc[2][2] = {{f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}};
+    for (int b = ch * cb; b < ch * cb + cb; b += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        wblock<KG, PK>(x[u], ob, acc, pacc);
+#pragma unroll
+        for (int g = 0; g < KG; ++g) x[u][g] = pa[(min(b + 2 + u, blast) * KG + g) * 64];
+      }
+    }
+    float r[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      r[t] = PK ? (pacc[t][0].x + pacc[t][0].y) + (pacc[t][1].x + pacc[t][1].y)
+                : (acc[t][0] + acc[t][1]) + (acc[t][2] + acc[t][3]);
+    tot += (double)reduce32(r, lane);
+  }
+  out[blockIdx.x * 64 + lane] = (float)tot;
+}
+
 static unsigned short bf16_bits(float v) {
   unsigned u;
   memcpy(&u, &v, 4);
@@ -304,7 +373,7 @@ int main() {
   const size_t n_pack = (size_t)NB16 * 64 * 8;       // bf16 elements: M points x 32 slots
   unsigned short* h = (unsigned short*)malloc(n_pack * 2);
   srand(1);
-  for (size_t i = 0; i < n_pack; ++i) h[i] = bf16_bits(-0.5f + (float)rand() / RAND_MAX);
+  for (size_t i = 0; i < n_pack; ++i) h[i] = bf16_bits(-0.5f + (float)rand() / (float)RAND_MAX);
   void* pack;
   float* out;
   CHECK(hipMalloc(&pack, n_pack * 2));
@@ -316,8 +385,9 @@ int main() {
   CHECK(hipEventCreate(&e1));
   struct V { const char* name; void (*fn)(const bf16x8*, float*, float); };
   V vs[] = {{"cur16", k_cur16}, {"u16", k_u16<false>}, {"s16", k_u16<true>},
-            {"s32", k_s32<true>}, {"p32", k_s32<false>}, {"s32k32", k_s32k32}};
-  const double pairs = (double)waves * 64 * M;
+            {"s32", k_s32<true>}, {"p32", k_s32<false>}, {"s32k32", k_s32k32},
+            {"w1s", k_walk<1, false>}, {"w1p", k_walk<1, true>}, {"w2s", k_walk<2, false>},
+            {"w2p", k_walk<2, true>}};
   const double peak = 8.0 * 1024 * 2.4e9;
   for (int rep = 0; rep < 2; ++rep) {
     for (auto& v : vs) {
@@ -330,6 +400,8 @@ int main() {
       float ms;
       CHECK(hipEventElapsedTime(&ms, e0, e1));
       ms /= n;
+      const bool half = v.name[0] == 'w' && v.name[1] == '2';   // K = 32: M / 2 points per byte budget
+      const double pairs = (double)waves * 64 * (half ? M / 2 : M);
       const double rate = pairs / (ms * 1e-3);
       printf("{\"variant\": \"%s\", \"rep\": %d, \"ms\": %.4f, \"Tpairs_s\": %.3f, \"frac_exp_peak\": %.4f}\n",
              v.name, rep, ms, rate / 1e12, rate / peak);

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--gibbs", action="store_true",
                     help="the Gibbs sweep table of scripts/jit_ab_gibbs.py (half-wave kind set 321)")
+    ap.add_argument("--outdir", default="exp", help="directory (under the repo) for the code objects")
     ap.add_argument("variants", nargs="+", help="name=space-separated extra options")
     a = ap.parse_args()
     if a.gibbs:
@@ -43,14 +44,14 @@ def main():
     km = plan.kind_mask | 128
     steps, ic, _ = plan.steps._vbn_host
     src = jit.plan_source(steps, ic, km)
-    os.makedirs(os.path.join(REPO, "exp"), exist_ok=True)
+    os.makedirs(os.path.join(REPO, a.outdir), exist_ok=True)
     base = jit.OPTIONS
     for v in a.variants:
         name, _, opts = v.partition("=")
         jit.OPTIONS = tuple(base) + tuple(opts.split())
         t0 = time.perf_counter()
         code = jit.compile_source(src)
-        out = os.path.join(REPO, "exp", f"plan_{a.config}_{name}.hsaco")
+        out = os.path.join(REPO, a.outdir, f"plan_{a.config}_{name}.hsaco")
         with open(out, "wb") as f:
             f.write(code)
         print(f"{out}: kind set {km}, {len(code)} B, {time.perf_counter() - t0:.1f} s")

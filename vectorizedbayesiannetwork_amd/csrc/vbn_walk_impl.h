@@ -1347,21 +1347,23 @@ __device__ __forceinline__ void bf16_split3(float v, __bf16 (&p)[3]) {
   p[2] = (__bf16)(r1 - (float)p[1]);
 }
 
-// slot k of the B operand: feature splits sp (_BF16_B pattern), -1 x 3, split of -|x'|^2, 0
-__device__ __forceinline__ __bf16 kde_bslot(int k, int nf, const __bf16 (&sp)[4][3], const __bf16 (&sx)[3]) {
+// slot k of the B operand: feature splits sp (_BF16_B pattern), -1 x 3, split of -|x'|^2 (zero
+// in the factored form: the A side's 1.0 slots then contribute nothing), 0
+__device__ __forceinline__ __bf16 kde_bslot(int k, int nf, const __bf16 (&sp)[4][3], const __bf16 (&sx)[3],
+                                            bool fform) {
   constexpr int pat[6] = {0, 0, 1, 0, 2, 1};
   const int f = k / 6;
   if (f < nf) return sp[f][pat[k - 6 * f]];
   const int r = k - 6 * nf;
   if (r < 3) return (__bf16)-1.f;
-  if (r < 6) return sx[r - 3];
+  if (r < 6 && !fform) return sx[r - 3];
   return (__bf16)0.f;
 }
 
 // the lane's particle side of tile t; -|x'|^2 exactly as kde_own accumulates it
 template <int KG>
 __device__ __forceinline__ void kde_b32_ops(const Lane& L, const int (&slots)[4], const float (&scl)[4], int nf,
-                                            KdeB32<KG>& o) {
+                                            bool fform, KdeB32<KG>& o) {
   const int h = L.lane >> 5, n = L.lane & 31;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -1378,7 +1380,8 @@ __device__ __forceinline__ void kde_b32_ops(const Lane& L, const int (&slots)[4]
     for (int g = 0; g < KG; ++g) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const __bf16 v0 = kde_bslot(16 * g + j, nf, sp, sx), v1 = kde_bslot(16 * g + 8 + j, nf, sp, sx);
+        const __bf16 v0 = kde_bslot(16 * g + j, nf, sp, sx, fform);
+        const __bf16 v1 = kde_bslot(16 * g + 8 + j, nf, sp, sx, fform);
         o.b[t][g][j] = h ? v1 : v0;
       }
     }
@@ -1407,17 +1410,31 @@ __device__ __forceinline__ void kde_b32_block(const bf16x8 (&a)[KG], const KdeB3
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
+    if constexpr (KG == 1) {
+      // f32x2 adds, one v_pk_add_f32 per two exps: 0.69 vs 0.63 of the exp-issue peak with
+      // plain adds (profiles/microbench/kde_pass1.hip w1p / w1s); beside the denser chained
+      // MFMAs of K = 32 they lose (w2p 0.57 vs w2s 0.59), so that form keeps plain adds
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[t][i & 3] += __builtin_amdgcn_exp2f(d[t][i]);
+      for (int i = 0; i < 16; i += 4) {
+        f32x2 p0 = f32x2{acc[t][0], acc[t][1]}, p1 = f32x2{acc[t][2], acc[t][3]};
+        p0 += f32x2{__builtin_amdgcn_exp2f(d[t][i]), __builtin_amdgcn_exp2f(d[t][i + 1])};
+        p1 += f32x2{__builtin_amdgcn_exp2f(d[t][i + 2]), __builtin_amdgcn_exp2f(d[t][i + 3])};
+        acc[t][0] = p0.x; acc[t][1] = p0.y; acc[t][2] = p1.x; acc[t][3] = p1.y;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i & 3] += __builtin_amdgcn_exp2f(d[t][i]);
+    }
   }
 }
 
-// block b's operands (clamped to the pack's last block; pa = pack + lane)
-template <int KG>
+// block b's operands (clamped to the pack's last block; pa = pack + lane; PG = the pack's K
+// groups per block: the factored form of two features reads group 0 of a K = 32 pack)
+template <int KG, int PG>
 __device__ __forceinline__ void kde_b32_load(const bf16x8* __restrict__ pa, int b, int blast, bf16x8 (&a)[KG]) {
   const int bb = KDE_BLK(min(b, blast));
 #pragma unroll
-  for (int g = 0; g < KG; ++g) a[g] = pa[(bb * KG + g) * 64];
+  for (int g = 0; g < KG; ++g) a[g] = pa[(bb * PG + g) * 64];
 }
 
 // Operands of the next KDE_PF blocks in flight (a ring of KDE_PF operand sets): block b's set
@@ -1429,15 +1446,15 @@ struct KdeTrip {
   bf16x8 x[KDE_PF][KG];
 };
 
-template <int KG>
+template <int KG, int PG>
 __device__ __forceinline__ void kde_b32_prefetch(const bf16x8* __restrict__ pa, int b0, int blast, KdeTrip<KG>& q) {
 #pragma unroll
-  for (int u = 0; u < KDE_PF; ++u) kde_b32_load<KG>(pa, b0 + u, blast, q.x[u]);
+  for (int u = 0; u < KDE_PF; ++u) kde_b32_load<KG, PG>(pa, b0 + u, blast, q.x[u]);
 }
 
 // per-lane tile partial sums of exp2(arg) over 32-point blocks [b0, b1), b1 - b0 a multiple of
 // KDE_PF (kde_cb)
-template <int KG>
+template <int KG, int PG>
 __device__ __forceinline__ void kde_b32_sums(const bf16x8* __restrict__ pa, int b0, int b1, int blast,
                                              const KdeB32<KG>& o, float (&s)[2], KdeTrip<KG>& q) {
   float acc[2][4];
@@ -1449,26 +1466,37 @@ __device__ __forceinline__ void kde_b32_sums(const bf16x8* __restrict__ pa, int 
 #pragma unroll
     for (int u = 0; u < KDE_PF; ++u) {
       kde_b32_block<KG>(q.x[u], o, acc);
-      kde_b32_load<KG>(pa, b + KDE_PF + u, blast, q.x[u]);
+      kde_b32_load<KG, PG>(pa, b + KDE_PF + u, blast, q.x[u]);
     }
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t) s[t] += (acc[t][0] + acc[t][1]) + (acc[t][2] + acc[t][3]);
 }
 
+// The factored form (round 5).  Sampling needs the chunk sums only up to a per-particle
+// factor, so they may be taken of exp2(2 x'.y' - |y'|^2) = 2^{|x'|^2} exp2(-|x' - y'|^2): the
+// contraction drops -|x'|^2's three slots and fits K = 16 for two features (6 nf + 3 = 15)
+// -- one MFMA per block instead of two chained ones, and the f32x2 adds (w1p, 0.69 vs w2s
+// 0.59 of the exp-issue peak).  The particle's sums are then shifted by s = -|x'|^2 relative to
+// the full form, and the record scan, the all-underflow rescue and the per-sample / per-query
+// pre-passes all work on a' = 2 x'.y' - |y'|^2 minus a shift sigma (0 here, |x'|^2 in the full
+// form, the largest a' after a rescue).  Used when every lane of the wave has |x'|^2 <=
+// KDE_FFORM_MAX (no overflow: sums <= M 2^{|x'|^2}); otherwise the full form.
+#define KDE_FFORM_MAX 96.f
+
 // Pass 1 of a node with nf features over its KDE_CHUNKS chunks: chunk sums -> scr[chunk][lane]
-template <int KG>
+template <int KG, int PG>
 __device__ __forceinline__ double kde_pass1(const bf16x8* __restrict__ pa, int cb32, const Lane& L,
-                                            const int (&slots)[4], const float (&scl)[4], int nf) {
+                                            const int (&slots)[4], const float (&scl)[4], int nf, bool fform) {
   KdeB32<KG> o;
-  kde_b32_ops<KG>(L, slots, scl, nf, o);
+  kde_b32_ops<KG>(L, slots, scl, nf, fform, o);
   const int blast = KDE_CHUNKS * cb32 - 1;
   KdeTrip<KG> q;
-  kde_b32_prefetch<KG>(pa, 0, blast, q);
+  kde_b32_prefetch<KG, PG>(pa, 0, blast, q);
   double tot = 0.0;
   for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
     float s[2] = {0.f, 0.f};
-    kde_b32_sums<KG>(pa, ch * cb32, ch * cb32 + cb32, blast, o, s, q);
+    kde_b32_sums<KG, PG>(pa, ch * cb32, ch * cb32 + cb32, blast, o, s, q);
     const float cs = kde_reduce_tiles(s, L.lane);
     L.scr[ch * WAVE + L.lane] = cs;
     tot += (double)cs;
@@ -1477,16 +1505,24 @@ __device__ __forceinline__ double kde_pass1(const bf16x8* __restrict__ pa, int c
 }
 
 // Sum over all nb32 blocks of a log-density pack (kde_logp_mfma)
-template <int KG>
+template <int KG, int PG>
 __device__ __forceinline__ float kde_sum_all(const bf16x8* __restrict__ pa, int nb32, const Lane& L,
-                                             const int (&slots)[4], const float (&scl)[4], int nf) {
+                                             const int (&slots)[4], const float (&scl)[4], int nf, bool fform) {
   KdeB32<KG> o;
-  kde_b32_ops<KG>(L, slots, scl, nf, o);
+  kde_b32_ops<KG>(L, slots, scl, nf, fform, o);
   KdeTrip<KG> q;
-  kde_b32_prefetch<KG>(pa, 0, nb32 - 1, q);
+  kde_b32_prefetch<KG, PG>(pa, 0, nb32 - 1, q);
   float s[2] = {0.f, 0.f};
-  kde_b32_sums<KG>(pa, 0, nb32, nb32 - 1, o, s, q);
+  kde_b32_sums<KG, PG>(pa, 0, nb32, nb32 - 1, o, s, q);
   return kde_reduce_tiles(s, L.lane);
+}
+
+// the form of a pack of nf features: K groups read (KG), K groups per block of the pack (PG)
+__device__ __forceinline__ float kde_sums_nf(const bf16x8* __restrict__ pa, int nb32, const Lane& L,
+                                             const int (&slots)[4], const float (&scl)[4], int nf, bool fform) {
+  if (nf == 1) return kde_sum_all<1, 1>(pa, nb32, L, slots, scl, nf, fform);
+  if (nf == 2 && fform) return kde_sum_all<1, 2>(pa, nb32, L, slots, scl, nf, fform);
+  return kde_sum_all<2, 2>(pa, nb32, L, slots, scl, nf, fform);
 }
 
 // Inverse-CDF scan of one chunk [j0, j1) (pass 2).  A lane whose threshold lies in the upper
@@ -1540,7 +1576,7 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   float xv[4] = {0.f, 0.f, 0.f, 0.f};
   const float negsq = kde_own(L, slots, scl, nf, xv);
   const bool pre = (st.flags & VBN_F_PRECOMP) != 0;
-  float shift = 0.f;
+  float shift = 0.f;                                  // sigma: the sums are of exp2(a' - sigma)
   if (pre) {                                          // pass 1 of this sample / query, pre-pass
     if (st.flags & VBN_F_PRECOMP_Q) {
       const cfloat* q = precomp_qrow(A, st, L);
@@ -1567,7 +1603,14 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
 #endif
   {
     const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
-    tot = nf == 1 ? kde_pass1<1>(pa, cb >> 1, L, slots, scl, nf) : kde_pass1<2>(pa, cb >> 1, L, slots, scl, nf);
+    const bool fform = __all(-negsq <= KDE_FFORM_MAX);
+    shift = fform ? 0.f : -negsq;
+    if (nf == 1)
+      tot = kde_pass1<1, 1>(pa, cb >> 1, L, slots, scl, nf, fform);
+    else if (nf == 2 && fform)
+      tot = kde_pass1<1, 2>(pa, cb >> 1, L, slots, scl, nf, fform);
+    else
+      tot = kde_pass1<2, 2>(pa, cb >> 1, L, slots, scl, nf, fform);
   }
   const int nfr = nf;                                 // replica form of the pass-1 elements
   const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
@@ -1575,14 +1618,14 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
   if (!pre && !(tot > 0.0)) {                         // every weight underflowed (or NaN parent)
     float amax = -INFINITY;
-    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nfr));
+    for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_rec(rec[j], xb0, xb1, xb2, 0.f, nfr));
     shift = amax;
     tot = 0.0;
     for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
       const int j0 = min(M, ch * cb * 16), j1 = min(M, j0 + cb * 16);
       float cs = 0.f;
       for (int j = j0; j < j1; ++j)
-        cs += __builtin_amdgcn_exp2f(kde_arg_rec(rec[j], xb0, xb1, xb2, negsq, nfr) - shift);
+        cs += __builtin_amdgcn_exp2f(kde_arg_rec(rec[j], xb0, xb1, xb2, 0.f, nfr) - shift);
       L.scr[ch * WAVE + lane] = cs;
       tot += (double)cs;
     }
@@ -1610,17 +1653,18 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   const float csum = L.scr[ch * WAVE + lane];
   const float4* __restrict__ rev = rec + (((M + 15) >> 4) * 16 + KDE_REC_TAIL);
   int idx;
-  // the replica chain per feature count, compile-time (kde_arg_rec)
+  // the replica chain a' = 2 x'.y' - |y'|^2 per feature count, compile-time (kde_arg_rec with
+  // no -|x'|^2 term: sigma carries it in the full form)
   if (nfr == 1)
     idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
-                   [&](const float4 r) { return fmaf(1.f, negsq, fmaf(r.y, -1.f, fmaf(r.x, xb0, 0.f))); });
+                   [&](const float4 r) { return fmaf(r.y, -1.f, fmaf(r.x, xb0, 0.f)); });
   else if (nfr == 2)
     idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift, [&](const float4 r) {
-      return fmaf(1.f, negsq, fmaf(r.z, -1.f, fmaf(r.y, xb1, fmaf(r.x, xb0, 0.f))));
+      return fmaf(r.z, -1.f, fmaf(r.y, xb1, fmaf(r.x, xb0, 0.f)));
     });
   else
     idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift, [&](const float4 r) {
-      return fmaf(r.w, -1.f, fmaf(r.z, xb2, fmaf(r.y, xb1, fmaf(r.x, xb0, negsq))));
+      return fmaf(r.w, -1.f, fmaf(r.z, xb2, fmaf(r.y, xb1, fmaf(r.x, xb0, 0.f))));
     });
   wave_sync();
   return idx;
@@ -1640,16 +1684,24 @@ __device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L,
   for (int f = 0; f < dp; ++f) slots[f] = L.ic[st.in_off + f];
   for (int d = 0; d < D; ++d) { slots[dp + d] = st.out_col + d; scl[dp + d] = c_y; }
   const int ny = dp + D;
+  // factored sums (kde_pass1) when no lane's |x'|^2 can overflow them: ln of a full-form sum =
+  // ln(factored sum) - |x'|^2 ln 2
+  float xv[4];
+  const float sq_y = -kde_own(L, slots, scl, ny, xv);
+  const float sq_p = root ? 0.f : -kde_own(L, slots, scl, dp, xv);
+  const bool fform = __all(sq_y <= KDE_FFORM_MAX);
   const bf16x8* __restrict__ pay = reinterpret_cast<const bf16x8*>(L.P + st.reserved[2]) + lane;
-  const float sy = ny == 1 ? kde_sum_all<1>(pay, nb32, L, slots, scl, ny) : kde_sum_all<2>(pay, nb32, L, slots, scl, ny);
+  const float sy = kde_sums_nf(pay, nb32, L, slots, scl, ny, fform);
   float sp = 1.f;
   if (!root) {
     const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
-    sp = dp == 1 ? kde_sum_all<1>(pa, nb32, L, slots, scl, dp) : kde_sum_all<2>(pa, nb32, L, slots, scl, dp);
+    sp = kde_sums_nf(pa, nb32, L, slots, scl, dp, fform);
   }
   wave_sync();
   if (!(sy > 0.f) || !(sp > 0.f)) return false;
-  lp += root ? (__logf(sy) + cy - log_n) : ((__logf(sy) - __logf(sp)) + cy);
+  constexpr float LN2 = 0.69314718055994531f;
+  const float corr = fform ? (root ? sq_y : sq_y - sq_p) * LN2 : 0.f;
+  lp += root ? ((__logf(sy) - corr) + cy - log_n) : (((__logf(sy) - __logf(sp)) - corr) + cy);
   return true;
 }
 
