@@ -391,10 +391,13 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
             precomp.record_stream(main)
         walk_plan = plan.pc
         pre_ran = True
-    # (the plan as given: a re-run of this launch repeats the pre-passes)
-    LAST_LAUNCH.update(pk=pk, plan=plan, fixed=fixed, b=b, n=n, fixed_per_particle=fixed_per_particle,
-                       noise=noise, state=state, seed=seed, offset=offset, plan_jit=plan_jit,
-                       precomputed=pre_ran, q_base=q_base)
+    # (the plan as given: a re-run of this launch repeats the pre-passes; a predicated launch --
+    # importance sampling's fallback re-draw -- is not recorded, so LAST_LAUNCH stays the walk
+    # whose outputs the call returns unless the fallback fired)
+    if run_if is None:
+        LAST_LAUNCH.update(pk=pk, plan=plan, fixed=fixed, b=b, n=n, fixed_per_particle=fixed_per_particle,
+                           noise=noise, state=state, seed=seed, offset=offset, plan_jit=plan_jit,
+                           precomputed=pre_ran, q_base=q_base)
     plan = walk_plan
     args = (plan.steps, plan.in_cols, pk.params, fixed, noise, plan.out_cols, b, n,
             plan.n_slots, plan.max_out, plan.fixed_ld, fixed_per_particle, noise_b,
