@@ -42,7 +42,7 @@
 
 #define WAVE 64
 #define KDE_CHUNKS 16
-#define KDE_REC_TAIL 8   // weight-0 record rows after the last point (plan.py KDE_REC_TAIL)
+#define KDE_REC_TAIL 16  // weight-0 record rows after the last point (plan.py KDE_REC_TAIL)
 #define LOG_2PI_F 1.8378770664093453f
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -1529,35 +1529,58 @@ __device__ __forceinline__ float kde_sums_nf(const bf16x8* __restrict__ pa, int 
 // half of its chunk scans backwards from the end for the right-hand mass csum - rem: the
 // point found is the same (the largest j with cum(j-1) <= rem), and no lane scans more than
 // about half a chunk.  Backward lanes walk the reversed record copy forward, so every lane
-// reads 4 consecutive records per trip with the next 4 in flight and no per-lane selects.
-// The weights are summed in scan order (bit-identical running sums to a point-by-point
-// scan); a crossing past the chunk end (rounding) is clamped to the chunk's last point.
-// rec: records (plan.py _kde_pack records=True), rev = reversed copy; M points.
+// reads 4 consecutive records per trip with the next trip's 4 in flight (two named record sets,
+// no register rotation) and no per-lane selects.  The weights exp2(arg(r)) (arg includes the
+// shift) are summed in scan order (bit-identical running sums to a point-by-point scan); one
+// compare per trip -- c > lim, with lim the float below the goal for backward lanes (c >= goal)
+// -- and the crossing inside the trip is located after the loop; a crossing past the chunk end
+// (rounding) is clamped to the chunk's last point.  rec: records (plan.py _kde_pack
+// records=True), rev = reversed copy; M points.  Against round 4's form (selects inside the
+// trip, a register rotation of the next records, the shift as a separate subtraction): cfg4
+// plan kernel without precompute 143 -> 137 ms; trips of 8 records lost (145 ms,
+// profiles/r05_bench/r05d_ab_scan.txt).
+// the largest float below x (x finite): the backward scan's c >= goal as c > float_below(goal)
+__device__ __forceinline__ float float_below(float x) {
+  const int i = __float_as_int(x);
+  return x > 0.f ? __int_as_float(i - 1) : (x == 0.f ? -__int_as_float(1) : __int_as_float(i + 1));
+}
+
 template <class ARG>
 __device__ __forceinline__ int kde_scan(const float4* __restrict__ rec, const float4* __restrict__ rev, int M,
-                                        int j0, int j1, float rem, float csum, float shift, ARG arg) {
+                                        int j0, int j1, float rem, float csum, ARG arg) {
   const bool back = rem > 0.5f * csum;
   const float goal = back ? csum - rem : rem;
+  const float lim = back ? float_below(goal) : goal;
   const float4* __restrict__ q = back ? rev + (M - j1) : rec + j0;
   const int n = j1 - j0;
-  int kh = n - 1;
-  float cs = 0.f;
-  float4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3];
-  for (int k = 0; k < n; k += 4) {
-    const float4 n0 = q[k + 4], n1 = q[k + 5], n2 = q[k + 6], n3 = q[k + 7];
-    const float c0 = cs + __builtin_amdgcn_exp2f(arg(r0) - shift);
-    const float c1 = c0 + __builtin_amdgcn_exp2f(arg(r1) - shift);
-    const float c2 = c1 + __builtin_amdgcn_exp2f(arg(r2) - shift);
-    const float c3 = c2 + __builtin_amdgcn_exp2f(arg(r3) - shift);
-    if (back ? c3 >= goal : c3 > goal) {
-      const int v = (back ? c0 >= goal : c0 > goal) ? 0
-                  : ((back ? c1 >= goal : c1 > goal) ? 1 : ((back ? c2 >= goal : c2 > goal) ? 2 : 3));
-      kh = min(k + v, n - 1);
-      break;
+  float cs = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+  int kt = n;                                   // first point of the crossing trip (n: none)
+  float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+  float4 b0 = q[4], b1 = q[5], b2 = q[6], b3 = q[7];
+  for (int k = 0; k < n; k += 8) {
+    {
+      const float e0 = cs + __builtin_amdgcn_exp2f(arg(a0));
+      const float e1 = e0 + __builtin_amdgcn_exp2f(arg(a1));
+      const float e2 = e1 + __builtin_amdgcn_exp2f(arg(a2));
+      const float e3 = e2 + __builtin_amdgcn_exp2f(arg(a3));
+      if (e3 > lim) { c0 = e0; c1 = e1; c2 = e2; c3 = e3; kt = k; break; }
+      cs = e3;
     }
-    cs = c3;
-    r0 = n0; r1 = n1; r2 = n2; r3 = n3;
+    a0 = q[k + 8]; a1 = q[k + 9]; a2 = q[k + 10]; a3 = q[k + 11];
+    if (k + 4 >= n) break;
+    {
+      const float e0 = cs + __builtin_amdgcn_exp2f(arg(b0));
+      const float e1 = e0 + __builtin_amdgcn_exp2f(arg(b1));
+      const float e2 = e1 + __builtin_amdgcn_exp2f(arg(b2));
+      const float e3 = e2 + __builtin_amdgcn_exp2f(arg(b3));
+      if (e3 > lim) { c0 = e0; c1 = e1; c2 = e2; c3 = e3; kt = k + 4; break; }
+      cs = e3;
+    }
+    b0 = q[k + 12]; b1 = q[k + 13]; b2 = q[k + 14]; b3 = q[k + 15];
   }
+  (void)c3;
+  const int v = c0 > lim ? 0 : (c1 > lim ? 1 : (c2 > lim ? 2 : 3));
+  const int kh = kt < n ? min(kt + v, n - 1) : n - 1;
   return min(max(back ? j1 - 1 - kh : j0 + kh, 0), M - 1);
 }
 
@@ -1655,16 +1678,18 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   int idx;
   // the replica chain a' = 2 x'.y' - |y'|^2 per feature count, compile-time (kde_arg_rec with
   // no -|x'|^2 term: sigma carries it in the full form)
+  // (the shift enters the chain as its addend: -0 in the factored form, so the same values)
+  const float nsh = -shift;
   if (nfr == 1)
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
-                   [&](const float4 r) { return fmaf(r.y, -1.f, fmaf(r.x, xb0, 0.f)); });
+    idx = kde_scan(rec, rev, M, j0, j1, rem, csum,
+                   [&](const float4 r) { return fmaf(r.y, -1.f, fmaf(r.x, xb0, nsh)); });
   else if (nfr == 2)
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift, [&](const float4 r) {
-      return fmaf(r.z, -1.f, fmaf(r.y, xb1, fmaf(r.x, xb0, 0.f)));
+    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, [&](const float4 r) {
+      return fmaf(r.z, -1.f, fmaf(r.y, xb1, fmaf(r.x, xb0, nsh)));
     });
   else
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift, [&](const float4 r) {
-      return fmaf(r.w, -1.f, fmaf(r.z, xb2, fmaf(r.y, xb1, fmaf(r.x, xb0, 0.f))));
+    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, [&](const float4 r) {
+      return fmaf(r.w, -1.f, fmaf(r.z, xb2, fmaf(r.y, xb1, fmaf(r.x, xb0, nsh))));
     });
   wave_sync();
   return idx;
@@ -1790,8 +1815,8 @@ __device__ __forceinline__ int kde_index_valu(const vbn_walk_args& A, const vbn_
   const float rem = (float)(thr - cum);
   const float csum = L.scr[ch * WAVE + lane];
   const float4* __restrict__ rev = rec + (((M + 15) >> 4) * 16 + KDE_REC_TAIL);
-  const int idx = kde_scan(rec, rev, M, j0, j1, rem, csum, shift,
-                           [&](const float4 r) { return kde_arg_valu<NF>(xv, r); });
+  const int idx = kde_scan(rec, rev, M, j0, j1, rem, csum,
+                           [&](const float4 r) { return kde_arg_valu<NF>(xv, r) - shift; });
   wave_sync();
   return idx;
 }

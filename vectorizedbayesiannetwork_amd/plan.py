@@ -42,7 +42,7 @@ STEP_INTS = 32
  S_WBLK_OFF, S_WBLK_LEN, S_RES7) = range(32)
 WBLK_CHUNK = 256          # floats per LDS-DMA wave instruction (64 lanes x 16 B)
 KDE_CHUNKS = 16
-KDE_REC_TAIL = 8       # weight-0 record rows after the last point (csrc kde_scan prefetch)
+KDE_REC_TAIL = 16      # weight-0 record rows after the last point (csrc kde_scan: two trips of 4 ahead)
 MLP_HIDDEN = (32, 32)
 # heads at least this wide run on the split-f16 MFMA (csrc head_mfma; cfg3 walk 2.97 -> 2.74 ms,
 # profiles/r03_bench/r03q_ab_cfg3.txt).  1 << 30 turns the MFMA head off.
