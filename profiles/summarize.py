@@ -5,7 +5,9 @@ HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
 on gfx950 FETCH_SIZE reads half the bytes of wide coalesced streaming reads (doubled here,
 flagged as an upper estimate for other access widths); WRITE_SIZE is exact for 16-B
 streaming stores and uncalibrated for the walk's 4-B-per-lane stores (reported as is).
-Usage: summarize.py <prof_dir> <out.json> [kernel_substring]
+Usage: summarize.py <prof_dir> <out.json> [kernel_substring] [min_grid]
+(min_grid: launches with fewer threads are ignored, default 4096 * 64: the full-size walks;
+the Gibbs sweep passes 1)
 (default: the plan-specialised walk vbn_walk_plan when the trace has it, else vbn_walk_kernel)
 """
 import collections
@@ -17,7 +19,8 @@ import sys
 def main():
     d, out = sys.argv[1], sys.argv[2]
     rows = list(csv.DictReader(open(f"{d}/trace/run_kernel_stats.csv")))
-    if len(sys.argv) > 3:
+    min_grid = int(sys.argv[4]) if len(sys.argv) > 4 else 4096 * 64
+    if len(sys.argv) > 3 and sys.argv[3] != "-":
         kname = sys.argv[3]
     else:
         kname = "vbn_walk_plan" if any("vbn_walk_plan" in r["Name"] for r in rows) else "vbn_walk_kernel"
@@ -28,14 +31,14 @@ def main():
                        max_ns=float(r["MaxNs"]), pct=float(r["Percentage"]))
     trace = list(csv.DictReader(open(f"{d}/trace/run_kernel_trace.csv")))
     big = [int(t["End_Timestamp"]) - int(t["Start_Timestamp"]) for t in trace
-           if kname in t["Kernel_Name"] and int(t.get("Grid_Size_X", 0) or 0) >= 4096 * 64]
+           if kname in t["Kernel_Name"] and int(t.get("Grid_Size_X", 0) or 0) >= min_grid]
     if big:
         res["avg_ns_full_size"] = sum(big) / len(big)
     pmc = collections.defaultdict(list)
     for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
         try:
             for r in csv.DictReader(open(f"{d}/{sub}/run_counter_collection.csv")):
-                if kname in r["Kernel_Name"] and int(r["Grid_Size"]) >= 4096 * 64:
+                if kname in r["Kernel_Name"] and int(r["Grid_Size"]) >= min_grid:
                     pmc[r["Counter_Name"]].append(float(r["Counter_Value"]))
         except FileNotFoundError:
             pass

@@ -93,8 +93,12 @@ def _world(group) -> Tuple[int, int]:
 class ShardedEngine:
     """Wrap an engine (``infer_posterior`` or ``sample``) for query-sharded multi-GPU runs."""
 
-    def __init__(self, engine, group=None, gather: bool = False, dst: int = 0, overlap: bool = False):
+    def __init__(self, engine, group=None, gather: bool = False, dst: int = 0, overlap: bool = False,
+                 force_collectives: bool = False):
         self.engine = engine
+        # issue the seed broadcast, flag all-reduce and gathers even in a world of one rank (an
+        # initialised process group of size 1: the RCCL code path on a one-GPU box, tests)
+        self.force_collectives = bool(force_collectives)
         self.group = group
         self.gather = bool(gather)
         self.dst = int(dst)
@@ -124,7 +128,7 @@ class ShardedEngine:
         if self._gen is None:                        # once: rank 0's draw, broadcast
             rank, world = _world(self.group)
             s = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
-            if world > 1:
+            if world > 1 or (self.force_collectives and dist.is_initialized()):
                 s = s.to(self._device())
                 dist.broadcast(s, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0,
                                group=self.group)
@@ -139,7 +143,7 @@ class ShardedEngine:
 
     def _flag_reducer(self):
         rank, world = _world(self.group)
-        if world == 1:
+        if world == 1 and not (self.force_collectives and dist.is_initialized()):
             return None
         dev = self._device()
 
@@ -158,7 +162,8 @@ class ShardedEngine:
     def _gather(self, t: torch.Tensor, n_total: int) -> Optional[torch.Tensor]:
         rank, world = _world(self.group)
         b0, b1 = shard_bounds(n_total, rank, world)
-        if world == 1 or t.shape[0] != b1 - b0:     # e.g. MCM root target: (1, S) on every rank
+        forced = self.force_collectives and dist.is_initialized()
+        if (world == 1 and not forced) or t.shape[0] != b1 - b0:   # e.g. MCM root target: (1, S)
             return t
         dev = self._device()
         q_max = -(-n_total // world)
