@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5 f: the other workloads' benches (driver form: 20 steps, 5 warmup) with CPU baselines,
-# and the Gibbs sampler bench
+# the cfg3 occupancy and cfg5 ablation A/Bs, and the 2-rank gloo rehearsal
 set -o pipefail
 mkdir -p gpurun_out
 T=${TAG:-r05f}
@@ -8,18 +8,11 @@ for c in cfg2 cfg3 anchor64 cfg5; do
   timeout -k 10 600 python -u bench.py --config $c --steps 20 --warmup 5 > gpurun_out/${T}_bench_$c.json 2>gpurun_out/${T}_bench_$c.err || { tail -30 gpurun_out/${T}_bench_$c.err; exit 1; }
   cat gpurun_out/${T}_bench_$c.json
 done
-timeout -k 10 400 python -u profiles/bench_gibbs.py > gpurun_out/${T}_gibbs_4096.json 2>gpurun_out/${T}_gibbs.err || { tail -30 gpurun_out/${T}_gibbs.err; exit 1; }
-cat gpurun_out/${T}_gibbs_4096.json
 # 2-rank rehearsal of the multi-GPU bench path (default workload cfg4) on one GPU over gloo
 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29533 bench.py --gpus 2 --dist-backend gloo --steps 10 --warmup 2 --no-cpu-baseline \
   > gpurun_out/${T}_gloo2.json 2> gpurun_out/${T}_gloo2.err || { tail -20 gpurun_out/${T}_gloo2.err; exit 1; }
 cat gpurun_out/${T}_gloo2.json
-# Gibbs sweep kernel: rocprofv3 stats + PMC
-bash profiles/profile_gibbs.sh gpurun_out/prof_gibbs || exit 1
-python3 profiles/summarize.py gpurun_out/prof_gibbs gpurun_out/${T}_gibbs_pmc.json vbn_walk_plan 1 > /dev/null || exit 1
-cp gpurun_out/prof_gibbs/trace/run_kernel_stats.csv gpurun_out/${T}_gibbs_kernel_stats.csv
-cat gpurun_out/${T}_gibbs_pmc.json
 # cfg3 at 3 waves per SIMD (no spills) against 4 (A/B code objects, ABAB)
 VBN_LIVENESS_ORDER=0 timeout -k 10 400 python -u scripts/jit_ab.py --config cfg3 abx5/plan_cfg3_base.hsaco abx5/plan_cfg3_wpe3.hsaco \
   abx5/plan_cfg3_base.hsaco abx5/plan_cfg3_wpe3.hsaco > gpurun_out/${T}_ab_cfg3.txt 2>&1 || { tail -20 gpurun_out/${T}_ab_cfg3.txt; exit 1; }

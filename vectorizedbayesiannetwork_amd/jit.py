@@ -87,8 +87,15 @@ def plan_source(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=No
                 first = False
             sweep.append("  __syncthreads();")
         sweep.append("}")
+    # lean production walks whose wide mdn / softmax_nn heads need more than 128 VGPRs (cfg3:
+    # 41 spills, ~0.8 GB of scratch traffic per launch at 4 waves per SIMD) run at 3 waves per
+    # SIMD without spills -- measured equal time (1.792 vs 1.794 ms, profiles/r05_bench/
+    # r05f_ab_cfg3.txt); KDE kind sets keep 4 waves (their exp stream needs the occupancy)
+    wpe = (["#define VBN_WPE 3"] if (kind_set & 128) and (kind_set & 20) and not (kind_set & 8) and not levels
+           else [])
     return "\n".join([
         "// plan-specialised walk (vectorizedbayesiannetwork_amd/jit.py)",
+        *wpe,
         '#include "vbn_walk_impl.h"',
         f"#define VBN_PLAN_N_STEPS {len(rows)}",
         *chain,
