@@ -58,7 +58,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--wave-particles", type=int, default=None, help="32 / 64 (default: the engine's choice)")
     ap.add_argument("--chain-waves", type=int, default=None,
-                    help="0..4: waves per chain workgroup of the specialised sweep (default: the engine's choice)")
+                    help="0..8: waves per chain workgroup of the specialised sweep (default: the engine's choice)")
     ap.add_argument("--plan-jit", choices=("auto", "on", "off"), default="auto",
                     help="plan-specialised sweep kernel (vectorizedbayesiannetwork_amd/jit.py) or the interpreter")
     args = ap.parse_args()
@@ -107,6 +107,7 @@ def main():
     launch(0)
     specialised = bool(ops.LAST_WALK.get("specialised"))
     chain_waves = int(ops.LAST_WALK.get("chain_waves") or 0)
+    wp = int(ops.LAST_WALK.get("wave_particles") or wp)
     stream = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 3
@@ -127,7 +128,7 @@ def main():
         "value": round(B * args.steps / el, 2), "unit": "queries/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1e3 * el / args.steps, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (cfg2 DAG/SEM/query generator; random-init CPD weights)",
+        "data": f"synthetic (cfg2 DAG/SEM/query generator; {cfg.get('model_origin', 'random-init')} CPDs)",
         "config": {"workload": "gibbs32: 32node-gaussian_nn-gibbs", "chains": B, "n_samples": args.n_samples,
                    "burn_in": args.burn_in, "n_steps": args.thin, "sweeps": iters, "candidates": 8,
                    "wave_particles": wp, "chain_waves": chain_waves,

@@ -124,8 +124,106 @@ def test_gibbs_levels_schedule(name, n_waves):
             assert len(levels) < len(groups) + 1                         # some updates run together
 
 
+def _cases(name):
+    if name == "cfg2":
+        import bench
+        cfg, model, target, ev = bench.build_model("cfg2")
+        return model, [{"query": {"target": target, "evidence": dict.fromkeys(ev), "do": {}}}]
+    fx = load_golden(name)
+    return model_from_checkpoint(fx["model"]), fx["cases"]
+
+
+@pytest.mark.parametrize("name", NAMES + ["cfg2"])
+@pytest.mark.parametrize("n_waves", [1, 2, 4])
+@pytest.mark.parametrize("split", [None, True])
+def test_gibbs_schedule_phases(name, n_waves, split):
+    """plan.gibbs_schedule: the phases run every step once, in the levels of gibbs_levels; a
+    split level runs LATENT, children, SELECT in successive phases, each step of an update
+    scoring into its own row, and the SELECT adds its rows in sweep order -- so the score each
+    SELECT sees is the sequential sweep's float32 sum, bit for bit (emulated here)."""
+    import numpy as np
+    model, cases = _cases(name)
+    pk = P.PackedModel(model, torch.device("cpu"))
+    for case in cases:
+        q = case["query"]
+        fixed = set(q["evidence"]) | set(q["do"])
+        gp = P.build_gibbs_plan(pk, latent=[n for n in model.topo if n not in fixed],
+                                fixed=[n for n in model.topo if n in fixed], target=q["target"])
+        rows, ic, _ = gp.steps._vbn_host
+        phases, n_rows = P.gibbs_schedule(rows, ic, n_waves, split=split)
+        assert all(len(ph) == n_waves for ph in phases)
+        ops = [(k, w, op) for k, ph in enumerate(phases) for w, wops in enumerate(ph) for op in wops]
+        assert sorted(op[1] for _, _, op in ops) == list(range(len(rows)))   # each step once
+        phase_of = {op[1]: k for k, _, op in ops}
+        groups, level, _ = P._gibbs_update_levels(rows, ic)
+        for (b, e), lv in zip(groups, level):
+            for (b2, e2), lv2 in zip(groups, level):
+                if lv < lv2:
+                    assert max(phase_of[i] for i in range(b, e)) < min(phase_of[i] for i in range(b2, e2))
+            whole = phase_of[b] == phase_of[e - 1]                        # one wave, register score
+            assert all((phase_of[i] == phase_of[b]) if whole else (phase_of[b] < phase_of[i] < phase_of[e - 1])
+                       for i in range(b + 1, e - 1))
+            if whole:
+                assert len({w for _, w, op in ops if b <= op[1] < e}) == 1
+        # float32 score emulation: random per-step terms, sequential vs scheduled
+        rng = np.random.default_rng(0)
+        term = rng.standard_normal(len(rows)).astype(np.float32) * np.float32(100)
+        seq, lp = {}, np.float32(0)
+        for i, r in enumerate(rows):
+            role = int(r[P.S_ROLE])
+            if role == P.ROLE_LATENT:
+                lp = np.float32(0) + term[i]
+            elif role == P.ROLE_FIXED:
+                lp = np.float32(lp + term[i])
+            elif role == P.ROLE_SELECT:
+                seq[i] = lp
+        lds = np.full(max(n_rows, 1), np.nan, np.float32)
+        reg = [np.float32(0)] * n_waves
+        got = {}
+        for ph in phases:
+            for w, wops in enumerate(ph):
+                for op in wops:
+                    i, role = op[1], int(rows[op[1]][P.S_ROLE])
+                    if op[0] == "lpout":
+                        assert role in (P.ROLE_LATENT, P.ROLE_FIXED)
+                        lds[op[2]] = np.float32(0) + term[i]
+                    elif op[0] == "select":
+                        t = lds[op[2][0]]
+                        for rr in op[2][1:]:
+                            t = np.float32(t + lds[rr])
+                        got[i] = t
+                    elif role == P.ROLE_LATENT:
+                        reg[w] = np.float32(0) + term[i]
+                    elif role == P.ROLE_FIXED:
+                        reg[w] = np.float32(reg[w] + term[i])
+                    elif role == P.ROLE_SELECT:
+                        got[i] = reg[w]
+        assert got.keys() == seq.keys()
+        assert all(got[i].tobytes() == seq[i].tobytes() for i in seq)
+        if split:
+            assert n_rows > 0 and not any(op[0] == "run" and int(rows[op[1]][P.S_ROLE]) != P.ROLE_COLLECT
+                                          for _, _, op in ops)
+
+
+def test_gibbs_schedule_splits_uneven_levels():
+    """The cost model splits cfg2's uneven levels on 4 waves and the modelled sweep shortens
+    (whole updates 24.15 step units, split where it pays 19.7; one wave stays whole)."""
+    model, cases = _cases("cfg2")
+    pk = P.PackedModel(model, torch.device("cpu"))
+    q = cases[0]["query"]
+    gp = P.build_gibbs_plan(pk, latent=[n for n in model.topo if n not in q["evidence"]],
+                            fixed=[n for n in model.topo if n in q["evidence"]], target=q["target"])
+    rows, ic, _ = gp.steps._vbn_host
+    whole = P.gibbs_schedule_cost(P.gibbs_schedule(rows, ic, 4, split=False)[0], rows)
+    auto, n_rows = P.gibbs_schedule(rows, ic, 4)
+    assert n_rows > 0 and P.gibbs_schedule_cost(auto, rows) < 0.85 * whole
+    one, n1 = P.gibbs_schedule(rows, ic, 1)
+    assert n1 == 0 and len(one) == len(P.gibbs_levels(rows, ic, 1))
+
+
 def test_chain_sweep_source():
-    """jit.plan_source with a level schedule: the chain-workgroup sweep, every step once."""
+    """jit.plan_source with a phased schedule: the chain-workgroup sweep, every step once."""
+    import re
     import bench
     from vectorizedbayesiannetwork_amd import jit
     cfg, model, target, ev = bench.build_model("cfg2")
@@ -133,11 +231,14 @@ def test_chain_sweep_source():
     gp = P.build_gibbs_plan(pk, latent=[n for n in model.topo if n not in ev],
                             fixed=[n for n in model.topo if n in ev], target=target)
     rows, ic, _ = gp.steps._vbn_host
-    levels = P.gibbs_levels(rows, ic, 4)
-    src = jit.plan_source(rows, ic, gp.kind_mask | 64 | 256, levels)
+    phases, n_rows = P.gibbs_schedule(rows, ic, 4)
+    src = jit.plan_source(rows, ic, gp.kind_mask | 64 | 256, (phases, n_rows))
     assert "#define VBN_PLAN_CHAIN_WAVES 4" in src
-    assert src.count("__syncthreads();") == len(levels)
-    import re
-    idx = [int(x) for seq in re.findall(r"vbn_seq<int, ([0-9, ]+)>", src) for x in seq.split(",")]
+    assert f"__shared__ float vbn_lp_rows[{n_rows} * WAVE];" in src
+    assert src.count("__syncthreads();") == len(phases)
+    idx = [int(x) for x in re.findall(r"vbn_plan_step_(?:direct|lpout|select)<KM, ([0-9]+)", src)]
     assert sorted(idx) == list(range(len(rows)))
     assert "VBN_PLAN_CHAIN_WAVES" not in jit.plan_source(rows, ic, gp.kind_mask | 64 | 256)
+    assert "__launch_bounds__(4 * WAVE)" in src
+    src8 = jit.plan_source(rows, ic, gp.kind_mask | 256, P.gibbs_schedule(rows, ic, 8))
+    assert "#define VBN_PLAN_CHAIN_WAVES 8" in src8 and "__launch_bounds__(8 * WAVE)" in src8

@@ -129,16 +129,20 @@ def test_specialised_gibbs_sweeps_bit_identical(wave_particles):
     assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("wave_particles", [32, 64])
-@pytest.mark.parametrize("chain_waves", [1, 2, 4])
-def test_chain_workgroup_gibbs_bit_identical(wave_particles, chain_waves):
-    """Gibbs sweeps on chain workgroups (plan.gibbs_levels: the waves of a workgroup split each
-    sweep's node updates by level): the chains equal the sequential interpreter's bit for bit,
-    production draws, several collected sweeps, chains that do not fill the last workgroup."""
+@pytest.mark.parametrize("wave_particles,chain_waves,split", [
+    (32, 1, ""), (32, 2, ""), (32, 4, ""), (64, 1, ""), (64, 2, ""), (64, 4, ""), (32, 2, "1"), (64, 4, "1"),
+    (32, 4, "0"), (64, 8, ""), (32, 8, "1")])
+def test_chain_workgroup_gibbs_bit_identical(wave_particles, chain_waves, split, monkeypatch):
+    """Gibbs sweeps on chain workgroups (plan.gibbs_schedule: the waves of a workgroup split each
+    sweep's node updates by level, and split uneven levels' updates into LATENT / children /
+    SELECT phases -- "1" forces every level split, "0" none): the chains equal the sequential
+    interpreter's bit for bit, production draws, several collected sweeps, chains that do not
+    fill the last workgroup."""
     from vectorizedbayesiannetwork_amd import jit, ops
     from vectorizedbayesiannetwork_amd.engines import GibbsSampler, Query
     if not jit.enabled():
         pytest.skip("VBN_PLAN_JIT=0")
+    monkeypatch.setenv("VBN_GIBBS_SPLIT", split)
     model, vbn, target, ev = synthetic_workload("cfg2", 13, "cuda")
     q = Query(target, {k: v.cuda() for k, v in ev.items()})
     outs = []
@@ -155,7 +159,7 @@ def test_chain_workgroup_gibbs_bit_identical(wave_particles, chain_waves):
 
 
 @pytest.mark.parametrize("name", ["ext_gibbs_mix10", "ext_gibbs_kde6"])
-def test_chain_workgroup_gibbs_against_oracle(name):
+def test_chain_workgroup_gibbs_against_oracle(name, monkeypatch):
     """Chain-workgroup sweeps with the reference's recorded draws injected (every CPD family of
     the fixtures: mixed kinds, KDE): the collected chains match the oracle and the reference's
     own outputs, and equal the sequential interpreter bit for bit."""
@@ -176,11 +180,13 @@ def test_chain_workgroup_gibbs_against_oracle(name):
         latent = [x for x in model.topo if x not in q["evidence"] and x not in q["do"]]
         noise = gibbs_noise(case, model, latent, max(model.out_dim(x) for x in model.topo))
         ref = GibbsSampler(n_samples=n, collect="chain", plan_jit=False, **p).sample(vbn, qq, n, _noise=noise)
-        e = GibbsSampler(n_samples=n, collect="chain", plan_jit=True, chain_waves=4, **p)
-        got = e.sample(vbn, qq, n, _noise=noise)
-        torch.cuda.synchronize()
-        assert ops.LAST_WALK.get("chain_waves") == 4, jit._failed
-        assert torch.equal(torch.nan_to_num(got, 7.0), torch.nan_to_num(ref, 7.0))
+        for split in ("", "1"):                      # cost-model schedule, every level split
+            monkeypatch.setenv("VBN_GIBBS_SPLIT", split)
+            e = GibbsSampler(n_samples=n, collect="chain", plan_jit=True, chain_waves=4, **p)
+            got = e.sample(vbn, qq, n, _noise=noise)
+            torch.cuda.synchronize()
+            assert ops.LAST_WALK.get("chain_waves") == 4, jit._failed
+            assert torch.equal(torch.nan_to_num(got, 7.0), torch.nan_to_num(ref, 7.0))
         rxc = O.gibbs(model, q["target"], q["evidence"], q["do"], n, O.ReplayDraws(case["draws"]),
                       copy_collected=True, **p)
         assert torch.allclose(got.cpu(), rxc, rtol=1e-5, atol=1e-5, equal_nan=True)

@@ -552,10 +552,13 @@ extern "C" int vbn_hip_module_unload(void* handle) {
   return e == hipSuccess ? 0 : fail((int)e, hipGetErrorString(e));
 }
 
+// chain workgroups run up to 8 waves (the jit.py sweep unit's launch bounds follow its wave count)
+#define CHAIN_MAX_WAVES 8
+
 extern "C" int vbn_hip_module_chain_waves(void* handle, int32_t n_waves) {
   vbn_plan_module* m = (vbn_plan_module*)handle;
-  if (!m || n_waves < 1 || n_waves > WG_MAX_WAVES)
-    return fail(VBN_E_ARGS, "vbn_hip_module_chain_waves: bad module or wave count (1..4)");
+  if (!m || n_waves < 1 || n_waves > CHAIN_MAX_WAVES)
+    return fail(VBN_E_ARGS, "vbn_hip_module_chain_waves: bad module or wave count (1..8)");
   m->chain_waves = n_waves;
   return 0;
 }
@@ -566,7 +569,11 @@ extern "C" int vbn_hip_walk_module(const void* handle, const vbn_walk_args* a, v
   walk_launch w;
   const int rc = walk_shape(a, &w);
   if (rc) return rc;
-  if (w.kmi != m->kmi || a->n_steps != m->n_steps)
+  // a Gibbs sweep without injected draws may run the draw-free (| 256) unit at full wave too:
+  // the interpreter instantiates | 256 for half waves only, a plan unit is compiled per set
+  // (full-wave cfg2 sweep: 97 VGPR spills with the injected-draw paths, none without)
+  const unsigned free_km = w.kmi | ((a->mode == VBN_MODE_GIBBS && !a->noise) ? 256u : 0u);
+  if ((m->kmi != w.kmi && m->kmi != free_km) || a->n_steps != m->n_steps)
     return fail(VBN_E_ARGS, "vbn_hip_walk_module: the launch does not match the compiled plan (kind set / steps)");
   if (m->chain_waves > 0) {
     // chain workgroups: every wave of a workgroup walks the same wp candidate lanes; one LDS

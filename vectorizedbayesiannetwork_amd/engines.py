@@ -840,17 +840,15 @@ class GibbsSampler(_EngineBase):
     at every collected sweep instead (burn-in, thinning by ``n_steps``) -- the Markov chain.
     """
 
-    # below this many candidate lanes (B x 8) the sweep launch runs half-wave (4 chains per
-    # wave64, include/vbn_hip.h wave_particles): 1536 full waves = 1.5 per SIMD
-    HALF_WAVE_BELOW = 1536 * 64
+    HALF_WAVE_BELOW = ops.HALF_WAVE_BELOW   # ops.gibbs_walk's automatic half-wave threshold
 
     def __init__(self, n_samples: int = 200, burn_in: int = 10, n_steps: int = 1, collect: str = "reference",
                  wave_particles: Optional[int] = None, chain_waves: Optional[int] = None, **kwargs):
         super().__init__(n_samples=n_samples, **kwargs)
         if wave_particles not in (None, 32, 64):
             raise ValueError(f"wave_particles must be None (auto), 32 or 64, got {wave_particles!r}")
-        if chain_waves not in (None, 0, 1, 2, 3, 4):
-            raise ValueError(f"chain_waves must be None (auto) or 0..4, got {chain_waves!r}")
+        if chain_waves not in (None, *range(9)):
+            raise ValueError(f"chain_waves must be None (auto) or 0..8, got {chain_waves!r}")
         self.wave_particles = wave_particles
         self.chain_waves = chain_waves    # specialised sweeps: waves splitting a chain group's updates
         self.burn_in = int(burn_in)
@@ -861,9 +859,9 @@ class GibbsSampler(_EngineBase):
         self.collect = collect
 
     def _wave_particles(self, b: int) -> int:
-        if self.wave_particles is not None:
-            return self.wave_particles
-        return 32 if b * 8 < self.HALF_WAVE_BELOW else 64
+        """32 / 64, or 0: ops.gibbs_walk chooses (full waves on chain workgroups, half waves
+        for small batches otherwise; ops.LAST_WALK["wave_particles"] says which ran)."""
+        return 0 if self.wave_particles is None else self.wave_particles
 
     def _gibbs_plan(self, pk: PackedModel, target: str, vals) -> GibbsPlan:
         model = pk.model

@@ -59,31 +59,55 @@ def enabled() -> bool:
     return os.environ.get("VBN_PLAN_JIT", "1") != "0"
 
 
-def plan_source(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=None) -> str:
-    """The translation unit of one plan-specialised walk (csrc/vbn_walk_plan.h).  ``levels``
-    (plan.gibbs_levels: per level, per wave, step ranges) makes it a Gibbs sweep on chain
-    workgroups of ``len(levels[0])`` waves."""
+def plan_source(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, schedule=None) -> str:
+    """The translation unit of one plan-specialised walk (csrc/vbn_walk_plan.h).  ``schedule``
+    (plan.gibbs_schedule: (phases, n_rows), per phase the ops of each wave) makes it a Gibbs
+    sweep on chain workgroups of ``len(phases[0])`` waves."""
     rows = []
     for r in np.asarray(steps, np.int32).reshape(-1, 32):
         v = [int(x) for x in r]
         rows.append("  {" + ", ".join(map(str, v[:24])) + ", {" + ", ".join(map(str, v[24:])) + "}},")
     ic = [int(x) for x in np.asarray(in_cols, np.int32).reshape(-1)] or [0]
     chain, sweep = [], []
-    if levels:
-        chain = [f"#define VBN_PLAN_CHAIN_WAVES {len(levels[0])}"]
-        sweep = ["template <unsigned KM>",
+    if schedule:
+        phases, n_rows = schedule
+        chain = [f"#define VBN_PLAN_CHAIN_WAVES {len(phases[0])}"]
+        # split levels (plan.gibbs_schedule): a LATENT / child step scores into its own LDS row
+        # (from 0), the SELECT step adds the rows in sweep order
+        sweep = [f"__shared__ float vbn_lp_rows[{max(int(n_rows), 1)} * WAVE];",
+                 "template <unsigned KM, int I, int ROW>",
+                 "__device__ __forceinline__ void vbn_plan_step_lpout(const vbn_walk_args& A, "
+                 "const float* __restrict__ params, Lane& L) {",
+                 "  float t = 0.f;",
+                 "  vbn_plan_step_direct<KM, I>(A, params, L, t);",
+                 "  vbn_lp_rows[ROW * WAVE + L.lane] = t;",
+                 "}",
+                 "template <unsigned KM, int I, int R0, int... R>",
+                 "__device__ __forceinline__ void vbn_plan_step_select(const vbn_walk_args& A, "
+                 "const float* __restrict__ params, Lane& L) {",
+                 "  float t = vbn_lp_rows[R0 * WAVE + L.lane];",
+                 "  ((t += vbn_lp_rows[R * WAVE + L.lane]), ...);",
+                 "  vbn_plan_step_direct<KM, I>(A, params, L, t);",
+                 "}",
+                 "template <unsigned KM>",
                  "__device__ __forceinline__ void vbn_plan_sweep_levels(const vbn_walk_args& A, "
                  "const float* __restrict__ params, int wave, Lane& L, float& lp) {"]
-        for lv, waves in enumerate(levels):
-            sweep.append(f"  // level {lv}")
+
+        def call(op):
+            if op[0] == "run":
+                return f"vbn_plan_step_direct<KM, {op[1]}>(A, params, L, lp);"
+            if op[0] == "lpout":
+                return f"vbn_plan_step_lpout<KM, {op[1]}, {op[2]}>(A, params, L);"
+            return f"vbn_plan_step_select<KM, {op[1]}, {', '.join(map(str, op[2]))}>(A, params, L);"
+
+        for k, waves in enumerate(phases):
+            sweep.append(f"  // phase {k}")
             first = True
-            for w, ranges in enumerate(waves):
-                idx = [i for b, e in ranges for i in range(b, e)]
-                if not idx:
+            for w, ops in enumerate(waves):
+                if not ops:
                     continue
-                seq = ", ".join(map(str, idx))
-                sweep.append(f"  {'if' if first else 'else if'} (wave == {w}) "
-                             f"vbn_plan_run<KM>(A, params, L, lp, vbn_seq<int, {seq}>{{}});")
+                body = " ".join(call(op) for op in ops)
+                sweep.append(f"  {'if' if first else 'else if'} (wave == {w}) {{ {body} }}")
                 first = False
             sweep.append("  __syncthreads();")
         sweep.append("}")
@@ -91,8 +115,10 @@ def plan_source(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=No
     # 41 spills, ~0.8 GB of scratch traffic per launch at 4 waves per SIMD) run at 3 waves per
     # SIMD without spills -- measured equal time (1.792 vs 1.794 ms, profiles/r05_bench/
     # r05f_ab_cfg3.txt); KDE kind sets keep 4 waves (their exp stream needs the occupancy)
-    wpe = (["#define VBN_WPE 3"] if (kind_set & 128) and (kind_set & 20) and not (kind_set & 8) and not levels
+    wpe = (["#define VBN_WPE 3"] if (kind_set & 128) and (kind_set & 20) and not (kind_set & 8) and not schedule
            else [])
+    # chain workgroups may run up to 8 waves (vbn_hip_module_chain_waves)
+    bounds = max(len(schedule[0][0]), 4) if schedule else "WG_MAX_WAVES"
     return "\n".join([
         "// plan-specialised walk (vectorizedbayesiannetwork_amd/jit.py)",
         *wpe,
@@ -105,7 +131,7 @@ def plan_source(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=No
         f"__constant__ int32_t VBN_PLAN_IC[{len(ic)}] = {{{', '.join(map(str, ic))}}};",
         '#include "vbn_walk_plan.h"',
         *sweep,
-        f'extern "C" __global__ void __launch_bounds__(WG_MAX_WAVES * WAVE) '
+        f'extern "C" __global__ void __launch_bounds__({bounds} * WAVE) '
         f"__attribute__((amdgpu_waves_per_eu(VBN_WPE))) {KERNEL}(const vbn_walk_args A, "
         f"const float* __restrict__ params) {{ if (A.run_if && *A.run_if == 0) return; "
         f"vbn_walk_plan_body<{int(kind_set)}u>(A, params); }}",
@@ -242,9 +268,9 @@ def _compile_store(src: str, key: str) -> bytes:
     return code
 
 
-def code_object(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, levels=None) -> Tuple[str, bytes]:
+def code_object(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, schedule=None) -> Tuple[str, bytes]:
     """(cache key, code object) of a plan, from the memory / disk cache or compiled."""
-    src = plan_source(steps, in_cols, kind_set, levels)
+    src = plan_source(steps, in_cols, kind_set, schedule)
     key = _source_key(src)
     code = _cached_code(key)
     if code is None:
@@ -301,9 +327,10 @@ def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_ind
     call, "background" starts a hiprtc compile on a daemon thread (the module is used by the first
     launch after it finishes; jit.wait_pending() joins), "never" only uses cached code.
     ``chain_waves`` > 0: a Gibbs sweep table run on chain workgroups of that many waves
-    (plan.gibbs_levels)."""
+    (plan.gibbs_schedule)."""
     global _warned
-    mk = (device_index, f"{plan_key}:{kind_set}:{chain_waves}")
+    split_env = os.environ.get("VBN_GIBBS_SPLIT", "") if chain_waves > 0 else ""
+    mk = (device_index, f"{plan_key}:{kind_set}:{chain_waves}:{split_env}")
     h = _modules.get(mk)
     if h is not None:
         return h
@@ -314,11 +341,13 @@ def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_ind
         if mk[1] in _failed:
             return None
         try:
-            levels = None
+            schedule = None
             if chain_waves > 0:
-                from .plan import gibbs_levels
-                levels = gibbs_levels(steps, in_cols, chain_waves)
-            src = plan_source(steps, in_cols, kind_set, levels)
+                from .plan import gibbs_schedule
+                # VBN_GIBBS_SPLIT=0/1 forces whole / split levels (ablation); unset: the cost model
+                split = {"0": False, "1": True}.get(split_env)
+                schedule = gibbs_schedule(steps, in_cols, chain_waves, split=split)
+            src = plan_source(steps, in_cols, kind_set, schedule)
             key = _source_key(src)
             code = _cached_code(key)
             if code is None:

@@ -226,6 +226,8 @@ def _plan_module(lib, a, steps, step_begin, step_end, work, plan_jit, device, ch
     km = lib.vbn_hip_walk_kind_set(ctypes.byref(a))
     if km <= 0:
         return None
+    if a.mode == MODE_GIBBS and not a.noise:
+        km |= 256           # the draw-free unit at full wave too (vbn_hip_walk_module)
     # auto: a compiled plan serves every launch size (bit-identical outputs, so the choice never
     # depends on how a batch is sharded); large launches start a missing compile in the background
     compile = "sync" if plan_jit == 2 else ("background" if work >= jit.JIT_MIN_PARTICLES else "never")
@@ -251,16 +253,18 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
                plan_jit: int = 1, chain_waves: int = -1) -> Tensor:
     """``iters`` Gibbs sweeps (gibbs.py:34-87) over B chains x 8 candidate lanes, started from
     ``state`` [n_slots + 1, B*8]; returns the collected target values [B, n_collect, out_dim].
-    ``wave_particles`` 32: half-wave launch (4 chains per wave64, include/vbn_hip.h).
+    ``wave_particles`` 32: half-wave launch (4 chains per wave64, include/vbn_hip.h); 0 = auto
+    (full waves on chain workgroups; half waves for fewer than HALF_WAVE_BELOW candidate lanes
+    otherwise).
     ``plan_jit`` as for :func:`walk` (0 interpreter, 1 auto, 2 always specialised).
-    ``chain_waves`` (specialised sweeps only): 1..4 = chain workgroups of that many waves that
-    split each sweep's node updates by level (plan.gibbs_levels; bit-identical chains), 0 = one
-    wave per chain group, -1 = auto (chain workgroups of 4 when the one-wave form would leave
-    fewer than 2 waves per SIMD, CHAIN_WAVES_BELOW)."""
-    if wave_particles not in (32, 64):
-        raise ValueError(f"vbn_hip::gibbs_walk: wave_particles must be 32 or 64, got {wave_particles}")
-    if not -1 <= chain_waves <= 4:
-        raise ValueError(f"vbn_hip::gibbs_walk: chain_waves must be -1 (auto) or 0..4, got {chain_waves}")
+    ``chain_waves`` (specialised sweeps only): 1..8 = chain workgroups of that many waves that
+    split each sweep's node updates by level (plan.gibbs_schedule; bit-identical chains), 0 = one
+    wave per chain group, -1 = auto (chain workgroups of CHAIN_WAVES when the one-wave form would
+    leave fewer than 2 waves per SIMD, CHAIN_WAVES_BELOW)."""
+    if wave_particles not in (0, 32, 64):
+        raise ValueError(f"vbn_hip::gibbs_walk: wave_particles must be 0 (auto), 32 or 64, got {wave_particles}")
+    if not -1 <= chain_waves <= 8:
+        raise ValueError(f"vbn_hip::gibbs_walk: chain_waves must be -1 (auto) or 0..8, got {chain_waves}")
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::gibbs_walk runs on the GPU only (no CPU fallback); "
@@ -317,32 +321,46 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
     a.gibbs_thin = thin
     a.n_noise = n_noise
     a.wbuf_floats = int(wbuf)
+    auto_wp = wave_particles == 0
+    if auto_wp:       # full waves wherever a chain workgroup may run (r05k: 4096 chains, 64 x 8 waves
+        # 101.6 ms, 32 x 4 117.0 ms); the one-wave forms keep half waves for small batches
+        cw_auto = chain_waves if chain_waves >= 0 else (CHAIN_WAVES if total // WAVE < CHAIN_WAVES_BELOW else 0)
+        wave_particles = 64 if cw_auto > 0 or total >= HALF_WAVE_BELOW else 32
     a.wave_particles = int(wave_particles)
     lib = _lib.load()
     with torch.cuda.device(device):
         stream = ctypes.c_void_p(_stream_handle(device))
         cw = chain_waves
         if cw < 0:
-            cw = 4 if total // wave_particles < CHAIN_WAVES_BELOW else 0
+            cw = CHAIN_WAVES if total // wave_particles < CHAIN_WAVES_BELOW else 0
         module = _plan_module(lib, a, steps, 0, int(steps.shape[0]), total * iters, plan_jit, device, cw)
+        if module is None and auto_wp and total < HALF_WAVE_BELOW:
+            a.wave_particles = 32                   # interpreter: half waves below HALF_WAVE_BELOW
         if module is not None:
             _lib.check(lib.vbn_hip_walk_module(ctypes.c_void_p(module), ctypes.byref(a), stream), "vbn_hip_walk_module")
         else:
             _lib.check(lib.vbn_hip_walk(ctypes.byref(a), stream), "vbn_hip_walk")
     LAST_WALK["specialised"] = module is not None
     LAST_WALK["chain_waves"] = cw if module is not None else 0
+    LAST_WALK["wave_particles"] = int(a.wave_particles)
     return x
 
 
 # Gibbs launches whose one-wave form has fewer waves than this (2 per SIMD on 1024 SIMDs) run
-# the specialised sweep on chain workgroups of 4 waves
+# the specialised sweep on chain workgroups of CHAIN_WAVES waves (r05k, 4096 chains: 8 waves
+# 101.6 ms, 4 waves 108.3 ms, full waves both)
 CHAIN_WAVES_BELOW = 2048
+CHAIN_WAVES = 8
+# below this many candidate lanes (B x 8) the one-wave sweep forms run half-wave (4 chains per
+# wave64): 1536 full waves = 1.5 per SIMD
+HALF_WAVE_BELOW = 1536 * 64
+WAVE = 64
 
 
 @gibbs_walk.register_fake
 def _gibbs_walk_fake(steps, in_cols, params, fixed, noise, state, n_queries, n_slots, max_out, fixed_ld,
                      noise_b, n_noise, dmax, out_dim, iters, burn_in, thin, q_base, seed, offset, kind_mask, wbuf=0,
-                     wave_particles=64, plan_jit=1, chain_waves=-1):
+                     wave_particles=0, plan_jit=1, chain_waves=-1):
     return params.new_empty((n_queries, (iters - burn_in + thin - 1) // thin, out_dim))
 
 

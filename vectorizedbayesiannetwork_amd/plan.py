@@ -861,6 +861,26 @@ def gibbs_levels(tab: np.ndarray, in_cols: np.ndarray, n_waves: int) -> List[Lis
     order.  A child's FIXED + KEEP step writes back the value it read (the same bits), which is
     a read for this analysis.
     """
+    groups, level, collect = _gibbs_update_levels(tab, in_cols)
+    n_lv = max(level) + 1 if level else 0
+    out: List[List[List[Tuple[int, int]]]] = []
+    for lv in range(n_lv):
+        mem = [g for g in range(len(groups)) if level[g] == lv]
+        load = [0] * n_waves
+        assign: List[List[int]] = [[] for _ in range(n_waves)]
+        for g in sorted(mem, key=lambda g: (-(groups[g][1] - groups[g][0]), g)):
+            w = min(range(n_waves), key=lambda w: (load[w], w))
+            assign[w].append(g)
+            load[w] += groups[g][1] - groups[g][0]
+        out.append([[groups[g] for g in sorted(a)] for a in assign])
+    if collect:
+        out.append([[(c, c + 1) for c in collect]] + [[] for _ in range(n_waves - 1)])
+    return out
+
+
+def _gibbs_update_levels(tab: np.ndarray, in_cols: np.ndarray):
+    """(groups, level, collect) of a Gibbs sweep table: the (begin, end) step range of every node
+    update, its level (gibbs_levels), and the COLLECT steps."""
     n = len(tab)
     groups: List[Tuple[int, int]] = []
     collect: List[int] = []
@@ -903,20 +923,87 @@ def gibbs_levels(tab: np.ndarray, in_cols: np.ndarray, n_waves: int) -> List[Lis
             if writes[h] & (reads[g] | writes[g]) or reads[h] & writes[g]:
                 lv = max(lv, level[h] + 1)
         level.append(lv)
+    return groups, level, collect
+
+
+# Relative costs of the sweep's operations for gibbs_schedule: a step with an MLP (or KDE
+# scan), a root step (a table lookup and one draw), a SELECT, a workgroup barrier.
+_GIBBS_COST_MLP, _GIBBS_COST_ROOT, _GIBBS_COST_SELECT, _GIBBS_COST_BARRIER = 1.0, 0.2, 0.15, 0.1
+
+
+def _gibbs_step_cost(r) -> float:
+    if int(r[S_ROLE]) == ROLE_SELECT:
+        return _GIBBS_COST_SELECT
+    heavy = int(r[S_WBLK_LEN]) > 0 or int(r[S_KIND]) == KIND_ID["kde"]
+    return _GIBBS_COST_MLP if heavy else _GIBBS_COST_ROOT
+
+
+def _lpt(items: Sequence[Tuple[float, object]], n_waves: int):
+    """Longest-processing-time assignment of (cost, item) to n_waves waves: (per-wave items in
+    input order, makespan)."""
+    load = [0.0] * n_waves
+    assign: List[List[int]] = [[] for _ in range(n_waves)]
+    for k in sorted(range(len(items)), key=lambda k: (-items[k][0], k)):
+        w = min(range(n_waves), key=lambda w: (load[w], w))
+        assign[w].append(k)
+        load[w] += items[k][0]
+    return [[items[k][1] for k in sorted(a)] for a in assign], max(load) if items else 0.0
+
+
+def gibbs_schedule(tab: np.ndarray, in_cols: np.ndarray, n_waves: int, split: Optional[bool] = None):
+    """Phased wave schedule of one Gibbs sweep table (csrc vbn_walk_plan.h, chain workgroups).
+
+    The levels are those of gibbs_levels.  A level runs in one of two forms, whichever the cost
+    model (_GIBBS_COST_*) says is shorter (``split`` forces one):
+
+    * whole updates: each wave runs whole LATENT .. SELECT groups, the score in its register,
+      then one barrier;
+    * split updates, for levels whose updates have uneven child counts: phase A runs the LATENT
+      steps, phase B every child log-prob step of the level, phase C the SELECT steps, each
+      phase balanced over the waves with a barrier after it.  A LATENT or child step starts its
+      own score at 0 and stores it in a score row (LDS); the SELECT step adds the rows in sweep
+      order -- ((lp_latent + lp_child1) + lp_child2) ..., the same additions as the sequential
+      sweep (each child adds one term), so the chains stay bit-identical.
+
+    Returns (phases, n_rows): ``phases`` is a list of per-wave op lists, a barrier after each
+    phase; an op is ("run", i) -- step i with the register score --, ("lpout", i, row) or
+    ("select", i, rows).  ``n_rows`` is the number of score rows the split levels need.
+    """
+    groups, level, collect = _gibbs_update_levels(tab, in_cols)
     n_lv = max(level) + 1 if level else 0
-    out: List[List[List[Tuple[int, int]]]] = []
+    phases: List[List[List[tuple]]] = []
+    n_rows = 0
     for lv in range(n_lv):
         mem = [g for g in range(len(groups)) if level[g] == lv]
-        load = [0] * n_waves
-        assign: List[List[int]] = [[] for _ in range(n_waves)]
-        for g in sorted(mem, key=lambda g: (-(groups[g][1] - groups[g][0]), g)):
-            w = min(range(n_waves), key=lambda w: (load[w], w))
-            assign[w].append(g)
-            load[w] += groups[g][1] - groups[g][0]
-        out.append([[groups[g] for g in sorted(a)] for a in assign])
+        whole_items = [(sum(_gibbs_step_cost(tab[i]) for i in range(*groups[g])), g) for g in mem]
+        whole, t_whole = _lpt(whole_items, n_waves)
+        t_whole += _GIBBS_COST_BARRIER
+        lat, kids, sel = [], [], []
+        row = 0
+        for g in mem:
+            b, e = groups[g]
+            rows = list(range(row, row + e - 1 - b))
+            row += e - 1 - b
+            lat.append((_gibbs_step_cost(tab[b]), ("lpout", b, rows[0])))
+            kids += [(_gibbs_step_cost(tab[i]), ("lpout", i, rows[i - b])) for i in range(b + 1, e - 1)]
+            sel.append((_gibbs_step_cost(tab[e - 1]), ("select", e - 1, tuple(rows))))
+        parts = [_lpt(ph, n_waves) for ph in (lat, kids, sel) if ph]
+        t_split = sum(t for _, t in parts) + _GIBBS_COST_BARRIER * len(parts)
+        use_split = split if split is not None else t_split < t_whole
+        if use_split:
+            phases += [p for p, _ in parts]
+            n_rows = max(n_rows, row)
+        else:
+            phases.append([[("run", i) for g in sorted(a) for i in range(*groups[g])] for a in whole])
     if collect:
-        out.append([[(c, c + 1) for c in collect]] + [[] for _ in range(n_waves - 1)])
-    return out
+        phases.append([[("run", c) for c in collect]] + [[] for _ in range(n_waves - 1)])
+    return phases, n_rows
+
+
+def gibbs_schedule_cost(phases, tab: np.ndarray) -> float:
+    """Modelled sweep time of a gibbs_schedule (the longest wave of each phase, plus barriers)."""
+    return sum(max(sum(_gibbs_step_cost(tab[op[1]]) for op in ops) for ops in ph) + _GIBBS_COST_BARRIER
+               for ph in phases)
 
 
 
