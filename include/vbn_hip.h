@@ -81,13 +81,15 @@ int vbn_hip_walk_module(const void* handle, const vbn_walk_args* args, void* str
 int vbn_hip_module_unload(void* handle);
 
 /* (ABI v8) Mark a loaded module as a Gibbs sweep compiled for chain workgroups of n_waves
- * (1..4) waves (csrc/vbn_walk_plan.h VBN_PLAN_CHAIN_WAVES; the host's level schedule,
- * vectorizedbayesiannetwork_amd/plan.py gibbs_levels): vbn_hip_walk_module then launches one
+ * (1..8) waves (csrc/vbn_walk_plan.h VBN_PLAN_CHAIN_WAVES; the host's phased schedule,
+ * vectorizedbayesiannetwork_amd/plan.py gibbs_schedule): vbn_hip_walk_module then launches one
  * workgroup of n_waves waves per 64 (half-wave: 32) candidate lanes, with one LDS copy of their
  * slots (n_slots rows) and n_waves x max(max_out, 1) scratch rows; the waves split each sweep's
- * node updates level by level.  Same outputs as the sequential sweep, bit for bit.  Only mode
- * GIBBS launches are accepted for such a module.  (Replaces the same reference call site as
- * the Gibbs walk: GibbsSampler.sample, vbn/sampling/gibbs.py:36-87.) */
+ * node updates level by level (and a split level's steps phase by phase).  Same outputs as the
+ * sequential sweep, bit for bit.  Only mode GIBBS launches are accepted for such a module; a
+ * launch without injected draws may run a module compiled for its kind set | 256 (draw-free).
+ * (Replaces the same reference call site as the Gibbs walk: GibbsSampler.sample,
+ * vbn/sampling/gibbs.py:36-87.) */
 int vbn_hip_module_chain_waves(void* handle, int32_t n_waves);
 
 /* Per-query weight normalisation over S particles.

@@ -1000,16 +1000,20 @@ __device__ __forceinline__ void step_mdn(const vbn_walk_args& A, const vbn_step&
   // pi = softmax(logits).clamp_min(1e-5); pi /= sum (mdn.py:227-228), computed once per
   // particle into the logit rows (the inverse CDF and the log-prob read pi_k repeatedly).
   // The two normalisations multiply by one reciprocal each (within an ulp of the reference's
-  // divisions; cfg3 walk -1.8 %)
+  // divisions; cfg3 walk -1.8 %); each exp is computed once and kept in its row
   auto make_pi = [&]() {
     lmax = -INFINITY;
     for (int k = 0; k < K; ++k) lmax = fmaxf(lmax, scr[k * WAVE + lane]);
     lsum = 0.f;
-    for (int k = 0; k < K; ++k) lsum += __expf(scr[k * WAVE + lane] - lmax);
+    for (int k = 0; k < K; ++k) {
+      const float e = __expf(scr[k * WAVE + lane] - lmax);
+      scr[k * WAVE + lane] = e;
+      lsum += e;
+    }
     psum = 0.f;
     const float rl = __builtin_amdgcn_rcpf(lsum);     // lsum >= 1
     for (int k = 0; k < K; ++k) {
-      const float p = fmaxf(__expf(scr[k * WAVE + lane] - lmax) * rl, 1e-5f);
+      const float p = fmaxf(scr[k * WAVE + lane] * rl, 1e-5f);
       scr[k * WAVE + lane] = p;
       psum += p;
     }
@@ -1128,7 +1132,18 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
     float m = -INFINITY;
     for (int c = 0; c < C; ++c) m = fmaxf(m, logit(c));
     float se = 0.f;
-    for (int c = 0; c < C; ++c) se += __expf(logit(c) - m);
+    // a latent non-root step without a log-prob reads the logits only here: each exp is
+    // computed once and kept in its row for the class probabilities below (same values)
+    const bool keep_e = latent && !root && !(st.flags & VBN_F_LOGP);
+    if (keep_e) {
+      for (int c = 0; c < C; ++c) {
+        const float e = __expf(logit(c) - m);
+        L.scr[(d * C + c) * WAVE + lane] = e;
+        se += e;
+      }
+    } else {
+      for (int c = 0; c < C; ++c) se += __expf(logit(c) - m);
+    }
     if (st.role == VBN_ROLE_PARAMS) {   // softmax(logits) per dim: [D][C] (RB target: D = 1)
       for (int c = 0; c < C; ++c) vwrite(L, st.out_col + d * C + c, __expf(logit(c) - m) / se);
       continue;
@@ -1139,12 +1154,12 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
     int idx;
     if (latent) {
       const float2 uu = d == 0 ? uu0 : draw_uniforms(A, st, d, L);
-      if (!root && !(st.flags & VBN_F_LOGP)) {
-        // the logits are not read again: the class probabilities replace them, computed once
+      if (keep_e) {
+        // the logits are not read again: the class probabilities replace the kept exps
         // (the inverse CDF reads each twice; same operations, so the same values); one
         // reciprocal of the sum instead of C divisions
         const float rse = __builtin_amdgcn_rcpf(se);  // se >= 1
-        for (int c = 0; c < C; ++c) L.scr[(d * C + c) * WAVE + lane] = __expf(logit(c) - m) * rse;
+        for (int c = 0; c < C; ++c) L.scr[(d * C + c) * WAVE + lane] = L.scr[(d * C + c) * WAVE + lane] * rse;
         idx = inv_cdf(C, uu.x, [&](int c) { return L.scr[(d * C + c) * WAVE + lane]; });
       } else {
         const float rse = __builtin_amdgcn_rcpf(se);  // se >= 1
@@ -1161,9 +1176,10 @@ __device__ __forceinline__ void step_softmax_nn(const vbn_walk_args& A, const vb
         if (mode == VBN_WITHIN_UNIFORM) {
           cont = left + uu.y * width;
         } else if (mode == VBN_WITHIN_TRIANGULAR) {
-          const float lv = left + width * sqrtf(fmaxf(uu.y * 0.5f, 0.0f));
-          const float rv = right - width * sqrtf(fmaxf((1.0f - uu.y) * 0.5f, 0.0f));
-          cont = uu.y < 0.5f ? lv : rv;
+          // only the chosen side's root (the same operations on the same values)
+          const bool lo = uu.y < 0.5f;
+          const float r = sqrtf(fmaxf((lo ? uu.y : 1.0f - uu.y) * 0.5f, 0.0f));
+          cont = lo ? left + width * r : right - width * r;
         } else {
           cont = center + draw_normal(A, st, d, L) * fmaxf(wscale * width, min_bw);
         }

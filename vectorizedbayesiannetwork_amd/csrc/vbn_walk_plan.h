@@ -182,10 +182,13 @@ __device__ __forceinline__ void vbn_walk_plan_general(const vbn_walk_args& A, co
 // the waves of a workgroup share ONE copy of their chains' slots in LDS and split each sweep's
 // node updates between them: the updates of one level touch no slot another one writes, so
 // they run at the same time on different waves, with one barrier per level (cfg2 DAG: 31
-// serial steps instead of 83 on 4 waves).  Every update runs the same device functions on the
-// same values with the same draws (keyed by node, chain and sweep) as in the sequential sweep,
-// so the chains are bit-identical to it.  Weights come from the blob (L1/L2): the waves run
-// different MLPs at once, so there is no per-workgroup staging.
+// serial steps instead of 83 on 4 waves).  Uneven levels run split (plan.gibbs_schedule): the
+// LATENT steps, then every child step, then the SELECTs, a barrier after each phase, the scores
+// passed through LDS rows (jit.py vbn_plan_step_lpout / _select) and added in sweep order.
+// Every update runs the same device functions on the same values with the same draws (keyed by
+// node, chain and sweep) as in the sequential sweep, so the chains are bit-identical to it.
+// Weights come from the blob (L1/L2): the waves run different MLPs at once, so there is no
+// per-workgroup staging.
 #ifdef VBN_PLAN_CHAIN_WAVES
 template <unsigned KM, int I>
 __device__ __forceinline__ void vbn_plan_step_direct(const vbn_walk_args& A, const float* __restrict__ params,
