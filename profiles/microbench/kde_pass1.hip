@@ -13,6 +13,9 @@
 //   s32k32    : K = 32 (3 features) as two chained 32x32x16 MFMAs per tile, plain adds
 //   w1s / w1p : the walk's round-5 form (a ring of 2 operand blocks), K = 16, plain / f32x2 adds
 //   w2s / w2p : the same with K = 32 (two chained MFMAs per tile and block), M / 2 points
+//   w1q / w1r / w2q / w2r : w1s / w1p / w2s / w2p software-pipelined (the next block's MFMAs
+//               issued before this block's exps)
+//   w1t / w1u / w2t / w2u : tile-pipelined (the next tile's MFMAs before this tile's exps)
 // Prints ms per launch and pair rate against the v_exp_f32 issue peak (8 cycles per wave64
 // instruction and SIMD, 1024 SIMDs, 2.4 GHz = 19.66 T/s).
 #include <hip/hip_runtime.h>
@@ -362,6 +365,151 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4)))
   out[blockIdx.x * 64 + lane] = (float)tot;
 }
 
+// ---- w<KG>q / w<KG>r: software-pipelined form: block b + 1's MFMAs are issued before block b's
+// exps, so no exp waits on its MFMA (q: plain adds, r: f32x2 adds) --------------------------------
+template <int KG>
+__device__ __forceinline__ void wmfma(const bf16x8 (&a)[KG], const bf16x8 (&ob)[2][KG], f32x16 (&d)[2]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x16 z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[i] = 0.f;
+    d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], ob[t][0], z, 0, 0, 0);
+    if constexpr (KG == 2) d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], ob[t][1], d[t], 0, 0, 0);
+  }
+}
+
+template <bool PK>
+__device__ __forceinline__ void wexps(const f32x16 (&d)[2], float (&acc)[2][4], f32x2 (&pacc)[2][2]) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if constexpr (PK) {
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        pacc[t][0] += f32x2{__builtin_amdgcn_exp2f(d[t][i]), __builtin_amdgcn_exp2f(d[t][i + 1])};
+        pacc[t][1] += f32x2{__builtin_amdgcn_exp2f(d[t][i + 2]), __builtin_amdgcn_exp2f(d[t][i + 3])};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i & 3] += __builtin_amdgcn_exp2f(d[t][i]);
+    }
+  }
+}
+
+template <int KG, bool PK>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_pipe(const bf16x8* __restrict__ pack, float* out, float seed) {
+  const int lane = threadIdx.x;
+  bf16x8 ob[2][KG];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int g = 0; g < KG; ++g) ob[t][g] = bop(lane, t + 2 * g, seed);
+  const bf16x8* __restrict__ pa = pack + lane;
+  const int nb = KG == 1 ? NB32 : NB32 / 2;
+  const int cb = nb / CHUNKS, blast = nb - 1;
+  bf16x8 x[2][KG];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int g = 0; g < KG; ++g) x[u][g] = pa[(min(u, blast) * KG + g) * 64];
+  f32x16 d[2], dn[2];
+  wmfma<KG>(x[0], ob, d);                                   // block 0
+#pragma unroll
+  for (int g = 0; g < KG; ++g) x[0][g] = pa[(min(2, blast) * KG + g) * 64];
+  double tot = 0.0;
+  for (int ch = 0; ch < CHUNKS; ++ch) {
+    float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x2 pacc[2][2] = {{f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}};
+    for (int b = ch * cb; b < ch * cb + cb; b += 2) {
+      // d = block b (issued before), x[1] = block b + 1, x[0] = block b + 2
+      wmfma<KG>(x[1], ob, dn);                              // block b + 1
+#pragma unroll
+      for (int g = 0; g < KG; ++g) x[1][g] = pa[(min(b + 3, blast) * KG + g) * 64];
+      wexps<PK>(d, acc, pacc);                              // block b
+      wmfma<KG>(x[0], ob, d);                               // block b + 2
+#pragma unroll
+      for (int g = 0; g < KG; ++g) x[0][g] = pa[(min(b + 4, blast) * KG + g) * 64];
+      wexps<PK>(dn, acc, pacc);                             // block b + 1
+    }
+    float r[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      r[t] = PK ? (pacc[t][0].x + pacc[t][0].y) + (pacc[t][1].x + pacc[t][1].y)
+                : (acc[t][0] + acc[t][1]) + (acc[t][2] + acc[t][3]);
+    tot += (double)reduce32(r, lane);
+  }
+  out[blockIdx.x * 64 + lane] = (float)tot;
+}
+
+// ---- w<KG>t / w<KG>u: tile-pipelined: tile i + 1's MFMAs are issued before tile i's exps
+// (two tile results live, as in the plain form; t: plain adds, u: f32x2 adds) ---------------------
+template <int KG>
+__device__ __forceinline__ f32x16 tmfma(const bf16x8 (&a)[KG], const bf16x8 (&b)[KG]) {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  f32x16 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], z, 0, 0, 0);
+  if constexpr (KG == 2) d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], d, 0, 0, 0);
+  return d;
+}
+
+template <bool PK>
+__device__ __forceinline__ void texps(const f32x16& d, float (&acc)[4], f32x2 (&pacc)[2]) {
+  if constexpr (PK) {
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+      pacc[0] += f32x2{__builtin_amdgcn_exp2f(d[i]), __builtin_amdgcn_exp2f(d[i + 1])};
+      pacc[1] += f32x2{__builtin_amdgcn_exp2f(d[i + 2]), __builtin_amdgcn_exp2f(d[i + 3])};
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i & 3] += __builtin_amdgcn_exp2f(d[i]);
+  }
+}
+
+template <int KG, bool PK>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_tpipe(const bf16x8* __restrict__ pack, float* out, float seed) {
+  const int lane = threadIdx.x;
+  bf16x8 ob[2][KG];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int g = 0; g < KG; ++g) ob[t][g] = bop(lane, t + 2 * g, seed);
+  const bf16x8* __restrict__ pa = pack + lane;
+  const int nb = KG == 1 ? NB32 : NB32 / 2;
+  const int cb = nb / CHUNKS, blast = nb - 1;
+  bf16x8 x[2][KG];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int g = 0; g < KG; ++g) x[u][g] = pa[(min(u, blast) * KG + g) * 64];
+  f32x16 dc = tmfma<KG>(x[0], ob[0]);                      // (block 0, tile 0)
+  double tot = 0.0;
+  for (int ch = 0; ch < CHUNKS; ++ch) {
+    float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f32x2 pacc[2][2] = {{f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}};
+    for (int b = ch * cb; b < ch * cb + cb; b += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // dc = (b + u, tile 0); x[u] = block b + u, x[u ^ 1] = block b + u + 1
+        const f32x16 dn = tmfma<KG>(x[u], ob[1]);          // (b + u, tile 1)
+#pragma unroll
+        for (int g = 0; g < KG; ++g) x[u][g] = pa[(min(b + u + 2, blast) * KG + g) * 64];
+        texps<PK>(dc, acc[0], pacc[0]);
+        dc = tmfma<KG>(x[u ^ 1], ob[0]);                    // (b + u + 1, tile 0)
+        texps<PK>(dn, acc[1], pacc[1]);
+      }
+    }
+    float r[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      r[t] = PK ? (pacc[t][0].x + pacc[t][0].y) + (pacc[t][1].x + pacc[t][1].y)
+                : (acc[t][0] + acc[t][1]) + (acc[t][2] + acc[t][3]);
+    tot += (double)reduce32(r, lane);
+  }
+  out[blockIdx.x * 64 + lane] = (float)tot;
+}
+
 static unsigned short bf16_bits(float v) {
   unsigned u;
   memcpy(&u, &v, 4);
@@ -387,7 +535,9 @@ int main() {
   V vs[] = {{"cur16", k_cur16}, {"u16", k_u16<false>}, {"s16", k_u16<true>},
             {"s32", k_s32<true>}, {"p32", k_s32<false>}, {"s32k32", k_s32k32},
             {"w1s", k_walk<1, false>}, {"w1p", k_walk<1, true>}, {"w2s", k_walk<2, false>},
-            {"w2p", k_walk<2, true>}};
+            {"w2p", k_walk<2, true>}, {"w1q", k_pipe<1, false>}, {"w1r", k_pipe<1, true>},
+            {"w2q", k_pipe<2, false>}, {"w2r", k_pipe<2, true>}, {"w1t", k_tpipe<1, false>},
+            {"w1u", k_tpipe<1, true>}, {"w2t", k_tpipe<2, false>}, {"w2u", k_tpipe<2, true>}};
   const double peak = 8.0 * 1024 * 2.4e9;
   for (int rep = 0; rep < 2; ++rep) {
     for (auto& v : vs) {
