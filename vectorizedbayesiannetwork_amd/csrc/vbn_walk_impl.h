@@ -1412,35 +1412,35 @@ __device__ __forceinline__ float kde_reduce_tiles(const float (&s)[2], int lane)
   return k + __shfl_xor(o, 32);
 }
 
-// one 32-point block: KG chained MFMAs per tile, 16 exps per tile summed into 4 accumulators
+// One tile of one 32-point block: KG chained MFMAs (C = 0)
 template <int KG>
-__device__ __forceinline__ void kde_b32_block(const bf16x8 (&a)[KG], const KdeB32<KG>& o, float (&acc)[2][4]) {
-  f32x16 d[2];
+__device__ __forceinline__ f32x16 kde_b32_tile(const bf16x8 (&a)[KG], const bf16x8 (&b)[KG]) {
+  f32x16 z;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    f32x16 z;
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  f32x16 d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], z, 0, 0, 0);
+  if constexpr (KG == 2) d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], d, 0, 0, 0);
+  return d;
+}
+
+// A tile's 16 exps summed into its 4 accumulators (in the order i = 0 .. 15, so the same sums
+// whatever the MFMA schedule)
+template <int KG>
+__device__ __forceinline__ void kde_b32_exps(const f32x16& d, float (&acc)[4]) {
+  if constexpr (KG == 1) {
+    // f32x2 adds, one v_pk_add_f32 per two exps: 0.69 vs 0.63 of the exp-issue peak with
+    // plain adds (profiles/microbench/kde_pass1.hip w1p / w1s); beside the denser chained
+    // MFMAs of K = 32 they gain nothing (w2u 0.600 vs w2t 0.597), so that form keeps plain adds
 #pragma unroll
-    for (int i = 0; i < 16; ++i) z[i] = 0.f;
-    d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], o.b[t][0], z, 0, 0, 0);
-    if constexpr (KG == 2) d[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], o.b[t][1], d[t], 0, 0, 0);
-  }
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    if constexpr (KG == 1) {
-      // f32x2 adds, one v_pk_add_f32 per two exps: 0.69 vs 0.63 of the exp-issue peak with
-      // plain adds (profiles/microbench/kde_pass1.hip w1p / w1s); beside the denser chained
-      // MFMAs of K = 32 they lose (w2p 0.57 vs w2s 0.59), so that form keeps plain adds
-#pragma unroll
-      for (int i = 0; i < 16; i += 4) {
-        f32x2 p0 = f32x2{acc[t][0], acc[t][1]}, p1 = f32x2{acc[t][2], acc[t][3]};
-        p0 += f32x2{__builtin_amdgcn_exp2f(d[t][i]), __builtin_amdgcn_exp2f(d[t][i + 1])};
-        p1 += f32x2{__builtin_amdgcn_exp2f(d[t][i + 2]), __builtin_amdgcn_exp2f(d[t][i + 3])};
-        acc[t][0] = p0.x; acc[t][1] = p0.y; acc[t][2] = p1.x; acc[t][3] = p1.y;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[t][i & 3] += __builtin_amdgcn_exp2f(d[t][i]);
+    for (int i = 0; i < 16; i += 4) {
+      f32x2 p0 = f32x2{acc[0], acc[1]}, p1 = f32x2{acc[2], acc[3]};
+      p0 += f32x2{__builtin_amdgcn_exp2f(d[i]), __builtin_amdgcn_exp2f(d[i + 1])};
+      p1 += f32x2{__builtin_amdgcn_exp2f(d[i + 2]), __builtin_amdgcn_exp2f(d[i + 3])};
+      acc[0] = p0.x; acc[1] = p0.y; acc[2] = p1.x; acc[3] = p1.y;
     }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i & 3] += __builtin_amdgcn_exp2f(d[i]);
   }
 }
 
@@ -1453,23 +1453,28 @@ __device__ __forceinline__ void kde_b32_load(const bf16x8* __restrict__ pa, int 
   for (int g = 0; g < KG; ++g) a[g] = pa[(bb * PG + g) * 64];
 }
 
-// Operands of the next KDE_PF blocks in flight (a ring of KDE_PF operand sets): block b's set
-// is used, then reloaded with block b + KDE_PF, so every load has KDE_PF - 1 blocks of exps in
-// front of its use.  The ring continues across calls (chunks) without a reload.
+// In flight across a node's blocks (and its chunks): the operands of the next KDE_PF blocks
+// (a ring: block b's set is reloaded with block b + KDE_PF once its last MFMA is issued) and
+// the tile-0 result of the next block.  The walk is tile-pipelined: tile i + 1's MFMAs are
+// issued before tile i's exps, so no exp waits on its MFMA (microbenchmark w1u 0.707 vs w1p
+// 0.690, w2t 0.597 vs w2s 0.588 of the exp-issue peak), with two tile results live as before.
 #define KDE_PF 2             // kde_cb keeps every chunk a multiple of 2 blocks of 32 points
 template <int KG>
 struct KdeTrip {
   bf16x8 x[KDE_PF][KG];
+  f32x16 d0;                 // tile 0 of the next block
 };
 
 template <int KG, int PG>
-__device__ __forceinline__ void kde_b32_prefetch(const bf16x8* __restrict__ pa, int b0, int blast, KdeTrip<KG>& q) {
+__device__ __forceinline__ void kde_b32_prefetch(const bf16x8* __restrict__ pa, int b0, int blast,
+                                                 const KdeB32<KG>& o, KdeTrip<KG>& q) {
 #pragma unroll
   for (int u = 0; u < KDE_PF; ++u) kde_b32_load<KG, PG>(pa, b0 + u, blast, q.x[u]);
+  q.d0 = kde_b32_tile<KG>(q.x[0], o.b[0]);
 }
 
 // per-lane tile partial sums of exp2(arg) over 32-point blocks [b0, b1), b1 - b0 a multiple of
-// KDE_PF (kde_cb)
+// KDE_PF (kde_cb); q holds block b0's tile 0 and the operands of blocks b0, b0 + 1
 template <int KG, int PG>
 __device__ __forceinline__ void kde_b32_sums(const bf16x8* __restrict__ pa, int b0, int b1, int blast,
                                              const KdeB32<KG>& o, float (&s)[2], KdeTrip<KG>& q) {
@@ -1481,8 +1486,11 @@ __device__ __forceinline__ void kde_b32_sums(const bf16x8* __restrict__ pa, int 
   for (int b = b0; b < b1; b += KDE_PF) {
 #pragma unroll
     for (int u = 0; u < KDE_PF; ++u) {
-      kde_b32_block<KG>(q.x[u], o, acc);
-      kde_b32_load<KG, PG>(pa, b + KDE_PF + u, blast, q.x[u]);
+      const f32x16 d1 = kde_b32_tile<KG>(q.x[u], o.b[1]);              // block b + u, tile 1
+      kde_b32_load<KG, PG>(pa, b + u + KDE_PF, blast, q.x[u]);
+      kde_b32_exps<KG>(q.d0, acc[0]);                                   // block b + u, tile 0
+      q.d0 = kde_b32_tile<KG>(q.x[(u + 1) % KDE_PF], o.b[0]);           // block b + u + 1, tile 0
+      kde_b32_exps<KG>(d1, acc[1]);
     }
   }
 #pragma unroll
@@ -1508,7 +1516,7 @@ __device__ __forceinline__ double kde_pass1(const bf16x8* __restrict__ pa, int c
   kde_b32_ops<KG>(L, slots, scl, nf, fform, o);
   const int blast = KDE_CHUNKS * cb32 - 1;
   KdeTrip<KG> q;
-  kde_b32_prefetch<KG, PG>(pa, 0, blast, q);
+  kde_b32_prefetch<KG, PG>(pa, 0, blast, o, q);
   double tot = 0.0;
   for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
     float s[2] = {0.f, 0.f};
@@ -1527,7 +1535,7 @@ __device__ __forceinline__ float kde_sum_all(const bf16x8* __restrict__ pa, int 
   KdeB32<KG> o;
   kde_b32_ops<KG>(L, slots, scl, nf, fform, o);
   KdeTrip<KG> q;
-  kde_b32_prefetch<KG, PG>(pa, 0, nb32 - 1, q);
+  kde_b32_prefetch<KG, PG>(pa, 0, nb32 - 1, o, q);
   float s[2] = {0.f, 0.f};
   kde_b32_sums<KG, PG>(pa, 0, nb32, nb32 - 1, o, s, q);
   return kde_reduce_tiles(s, L.lane);
