@@ -135,12 +135,14 @@ def _cases(name):
 
 @pytest.mark.parametrize("name", NAMES + ["cfg2"])
 @pytest.mark.parametrize("n_waves", [1, 2, 4])
-@pytest.mark.parametrize("split", [None, True])
+@pytest.mark.parametrize("split", [None, True, "dag"])
 def test_gibbs_schedule_phases(name, n_waves, split):
-    """plan.gibbs_schedule: the phases run every step once, in the levels of gibbs_levels; a
-    split level runs LATENT, children, SELECT in successive phases, each step of an update
-    scoring into its own row, and the SELECT adds its rows in sweep order -- so the score each
-    SELECT sees is the sequential sweep's float32 sum, bit for bit (emulated here)."""
+    """plan.gibbs_schedule: the phases run every step once and every ordering constraint of
+    plan.gibbs_step_deps holds (checked against an independent restatement: a step before
+    another = an earlier phase, or the same wave earlier in the same phase); the level forms
+    keep gibbs_levels' levels; a split step scores into its own row and the SELECT adds its
+    rows in sweep order -- so the score each SELECT sees is the sequential sweep's float32 sum,
+    bit for bit (emulated here)."""
     import numpy as np
     model, cases = _cases(name)
     pk = P.PackedModel(model, torch.device("cpu"))
@@ -155,16 +157,39 @@ def test_gibbs_schedule_phases(name, n_waves, split):
         ops = [(k, w, op) for k, ph in enumerate(phases) for w, wops in enumerate(ph) for op in wops]
         assert sorted(op[1] for _, _, op in ops) == list(range(len(rows)))   # each step once
         phase_of = {op[1]: k for k, _, op in ops}
+        pos = {op[1]: (k, w, j) for k, ph in enumerate(phases) for w, wops in enumerate(ph)
+               for j, op in enumerate(wops)}
+
+        def before(a, b):
+            (ka, wa, ja), (kb, wb, jb) = pos[a], pos[b]
+            return ka < kb or (ka == kb and wa == wb and ja < jb)
+
         groups, level, _ = P._gibbs_update_levels(rows, ic)
-        for (b, e), lv in zip(groups, level):
-            for (b2, e2), lv2 in zip(groups, level):
-                if lv < lv2:
-                    assert max(phase_of[i] for i in range(b, e)) < min(phase_of[i] for i in range(b2, e2))
+        # independent restatement of the constraints: per update pair h < g, through the slots
+        for g, (b, e) in enumerate(groups):
+            assert all(before(b, i) for i in range(b + 1, e)) and all(before(i, e - 1) for i in range(b, e - 1))
+            rd_g = [set(_group_rw(rows, ic, i, i + 1)[0]) if rows[i][P.S_ROLE] != P.ROLE_SELECT else set()
+                    for i in range(b, e)]
+            wg = _group_rw(rows, ic, b, e)[1]
+            for bh, eh in groups[:g]:
+                wh = _group_rw(rows, ic, bh, eh)[1]
+                for k, i in enumerate(range(b, e)):
+                    if rd_g[k] & wh:
+                        assert before(eh - 1, i), (i, eh - 1)
+                for i in range(bh, eh):
+                    if rows[i][P.S_ROLE] != P.ROLE_SELECT and _group_rw(rows, ic, i, i + 1)[0] & wg:
+                        assert before(i, b), (i, b)
+            assert P.gibbs_step_deps(rows, ic)[e - 1] >= set(range(b, e - 1))
+        if split is True:                                   # the level form keeps the levels
+            for (b, e), lv in zip(groups, level):
+                for (b2, e2), lv2 in zip(groups, level):
+                    if lv < lv2:
+                        assert max(phase_of[i] for i in range(b, e)) < min(phase_of[i] for i in range(b2, e2))
+        for b, e in groups:
             whole = phase_of[b] == phase_of[e - 1]                        # one wave, register score
-            assert all((phase_of[i] == phase_of[b]) if whole else (phase_of[b] < phase_of[i] < phase_of[e - 1])
-                       for i in range(b + 1, e - 1))
             if whole:
                 assert len({w for _, w, op in ops if b <= op[1] < e}) == 1
+                assert all(op[0] == "run" for _, _, op in ops if b <= op[1] < e)
         # float32 score emulation: random per-step terms, sequential vs scheduled
         rng = np.random.default_rng(0)
         term = rng.standard_normal(len(rows)).astype(np.float32) * np.float32(100)
@@ -200,7 +225,7 @@ def test_gibbs_schedule_phases(name, n_waves, split):
                         got[i] = reg[w]
         assert got.keys() == seq.keys()
         assert all(got[i].tobytes() == seq[i].tobytes() for i in seq)
-        if split:
+        if split in (True, "dag"):
             assert n_rows > 0 and not any(op[0] == "run" and int(rows[op[1]][P.S_ROLE]) != P.ROLE_COLLECT
                                           for _, _, op in ops)
 

@@ -131,11 +131,12 @@ def test_specialised_gibbs_sweeps_bit_identical(wave_particles):
 
 @pytest.mark.parametrize("wave_particles,chain_waves,split", [
     (32, 1, ""), (32, 2, ""), (32, 4, ""), (64, 1, ""), (64, 2, ""), (64, 4, ""), (32, 2, "1"), (64, 4, "1"),
-    (32, 4, "0"), (64, 8, ""), (32, 8, "1"), (64, 0, ""), (32, 0, "")])
+    (32, 4, "0"), (64, 8, ""), (32, 8, "1"), (64, 0, ""), (32, 0, ""), (64, 8, "levels"), (32, 2, "dag")])
 def test_chain_workgroup_gibbs_bit_identical(wave_particles, chain_waves, split, monkeypatch):
     """Gibbs sweeps on chain workgroups (plan.gibbs_schedule: the waves of a workgroup split each
     sweep's node updates by level, and split uneven levels' updates into LATENT / children /
-    SELECT phases -- "1" forces every level split, "0" none; chain_waves 0: the specialised
+    SELECT phases -- "1" forces every level split, "0" none, "levels" the per-level choice, "dag"
+    the step-level schedule, "" the cost model's pick; chain_waves 0: the specialised
     one-wave sweep, which at full wave runs the draw-free unit too): the chains equal the
     sequential interpreter's bit for bit, production draws, several collected sweeps, chains
     that do not fill the last workgroup."""

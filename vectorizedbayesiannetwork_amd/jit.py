@@ -344,8 +344,9 @@ def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_ind
             schedule = None
             if chain_waves > 0:
                 from .plan import gibbs_schedule
-                # VBN_GIBBS_SPLIT=0/1 forces whole / split levels (ablation); unset: the cost model
-                split = {"0": False, "1": True}.get(split_env)
+                # VBN_GIBBS_SPLIT=0/1/levels/dag: whole / split / per-level choice / the step-level schedule
+                # (ablation); unset: the cost model
+                split = {"0": False, "1": True, "dag": "dag", "levels": "levels"}.get(split_env)
                 schedule = gibbs_schedule(steps, in_cols, chain_waves, split=split)
             src = plan_source(steps, in_cols, kind_set, schedule)
             key = _source_key(src)

@@ -950,7 +950,94 @@ def _lpt(items: Sequence[Tuple[float, object]], n_waves: int):
     return [[items[k][1] for k in sorted(a)] for a in assign], max(load) if items else 0.0
 
 
-def gibbs_schedule(tab: np.ndarray, in_cols: np.ndarray, n_waves: int, split: Optional[bool] = None):
+def gibbs_step_deps(tab: np.ndarray, in_cols: np.ndarray):
+    """Step-level ordering constraints of a Gibbs sweep table: {step: set of steps that must run
+    before it} over the LATENT / child / SELECT steps (COLLECT steps excluded).
+
+    Inside an update, its children follow its LATENT step and its SELECT follows both.  Between
+    updates h < g (sweep order), with slot(u) the slots update u writes (candidates at its LATENT
+    step, the choice at its SELECT): a step of g that reads slot(h) runs after h's SELECT, and a
+    step of h that reads slot(g) runs before g's LATENT -- so every read sees the value the
+    sequential sweep gives it (a child's KEEP write-back rewrites the bits it read: a read)."""
+    groups, _, _ = _gibbs_update_levels(tab, in_cols)
+
+    def cols(r):
+        return set(range(int(r[S_OUTCOL]), int(r[S_OUTCOL]) + int(r[S_OUTDIM])))
+
+    def reads(i):
+        r = tab[i]
+        if int(r[S_ROLE]) == ROLE_SELECT:
+            return set()
+        rd = set(int(c) for c in in_cols[int(r[S_INOFF]):int(r[S_INOFF]) + int(r[S_NIN])])
+        return rd | cols(r) if int(r[S_ROLE]) == ROLE_FIXED else rd
+
+    rd = {i: reads(i) for b, e in groups for i in range(b, e)}
+    deps = {i: set() for i in rd}
+    for b, e in groups:
+        for i in range(b + 1, e):
+            deps[i].add(b)
+        deps[e - 1] |= set(range(b + 1, e - 1))
+    for g, (b, e) in enumerate(groups):
+        wg = cols(tab[b])
+        for bh, eh in groups[:g]:
+            wh = cols(tab[bh])
+            for i in range(b, e):
+                if rd[i] & wh:
+                    deps[i].add(eh - 1)
+            for i in range(bh, eh):
+                if rd[i] & wg:
+                    deps[b].add(i)
+    return deps
+
+
+def _gibbs_schedule_dag(tab: np.ndarray, in_cols: np.ndarray, n_waves: int):
+    """Phases of any ready steps (gibbs_step_deps), not whole levels: each phase fills the waves
+    with the ready steps of the longest remaining path first, up to a per-wave budget; the budget
+    with the shortest modelled sweep wins.  Every LATENT / child step scores into its own row."""
+    deps = gibbs_step_deps(tab, in_cols)
+    cost = {i: _gibbs_step_cost(tab[i]) for i in deps}
+    succ = {i: [] for i in deps}
+    for j, d in deps.items():
+        for i in d:
+            succ[i].append(j)
+    cp: Dict[int, float] = {}
+    for i in sorted(deps, reverse=True):          # a step's successors come later in the table
+        cp[i] = cost[i] + max((cp[j] for j in succ[i]), default=0.0)
+    groups, _, collect = _gibbs_update_levels(tab, in_cols)
+    row_of, n_rows, sel_rows = {}, 0, {}
+    for b, e in groups:
+        rows = []
+        for i in range(b, e - 1):
+            row_of[i] = n_rows
+            rows.append(n_rows)
+            n_rows += 1
+        sel_rows[e - 1] = tuple(rows)
+    best = None
+    for budget in (0.8, 1.0, 1.2, 1.4, 2.0, 3.0, float("inf")):
+        done, phases, t = set(), [], 0.0
+        while len(done) < len(deps):
+            ready = sorted((i for i in deps if i not in done and deps[i] <= done), key=lambda i: (-cp[i], i))
+            load = [0.0] * n_waves
+            waves: List[List[int]] = [[] for _ in range(n_waves)]
+            for i in ready:
+                w = min(range(n_waves), key=lambda w: (load[w], w))
+                if load[w] > 0 and load[w] + cost[i] > budget + 1e-9:
+                    continue
+                load[w] += cost[i]
+                waves[w].append(i)
+            done |= {i for ws in waves for i in ws}
+            t += max(load) + _GIBBS_COST_BARRIER
+            phases.append([[("select", i, sel_rows[i]) if i in sel_rows else ("lpout", i, row_of[i])
+                            for i in sorted(ws)] for ws in waves])
+        if best is None or t < best[0] - 1e-9:
+            best = (t, phases)
+    phases = best[1]
+    if collect:
+        phases.append([[("run", c) for c in collect]] + [[] for _ in range(n_waves - 1)])
+    return phases, n_rows
+
+
+def gibbs_schedule(tab: np.ndarray, in_cols: np.ndarray, n_waves: int, split=None):
     """Phased wave schedule of one Gibbs sweep table (csrc vbn_walk_plan.h, chain workgroups).
 
     The levels are those of gibbs_levels.  A level runs in one of two forms, whichever the cost
@@ -965,10 +1052,20 @@ def gibbs_schedule(tab: np.ndarray, in_cols: np.ndarray, n_waves: int, split: Op
       order -- ((lp_latent + lp_child1) + lp_child2) ..., the same additions as the sequential
       sweep (each child adds one term), so the chains stay bit-identical.
 
+    ``split="levels"`` keeps the per-level choice without the step-level form.
+    ``split="dag"`` (and the default, when its modelled sweep is shorter) drops the levels:
+    _gibbs_schedule_dag fills each phase with any steps whose constraints (gibbs_step_deps)
+    are met, longest remaining path first.
+
     Returns (phases, n_rows): ``phases`` is a list of per-wave op lists, a barrier after each
     phase; an op is ("run", i) -- step i with the register score --, ("lpout", i, row) or
-    ("select", i, rows).  ``n_rows`` is the number of score rows the split levels need.
+    ("select", i, rows).  ``n_rows`` is the number of score rows the split steps need.
     """
+    if split == "dag":
+        return _gibbs_schedule_dag(tab, in_cols, n_waves)
+    try_dag = split is None
+    if split == "levels":                 # the level forms only, chosen per level by the model
+        split = None
     groups, level, collect = _gibbs_update_levels(tab, in_cols)
     n_lv = max(level) + 1 if level else 0
     phases: List[List[List[tuple]]] = []
@@ -997,6 +1094,10 @@ def gibbs_schedule(tab: np.ndarray, in_cols: np.ndarray, n_waves: int, split: Op
             phases.append([[("run", i) for g in sorted(a) for i in range(*groups[g])] for a in whole])
     if collect:
         phases.append([[("run", c) for c in collect]] + [[] for _ in range(n_waves - 1)])
+    if try_dag and n_waves > 1:
+        dag = _gibbs_schedule_dag(tab, in_cols, n_waves)
+        if gibbs_schedule_cost(dag[0], tab) < gibbs_schedule_cost(phases, tab) - 1e-9:
+            return dag
     return phases, n_rows
 
 
