@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -1013,7 +1014,8 @@ def _gibbs_schedule_dag(tab: np.ndarray, in_cols: np.ndarray, n_waves: int):
             n_rows += 1
         sel_rows[e - 1] = tuple(rows)
     best = None
-    for budget in (0.8, 1.0, 1.2, 1.4, 2.0, 3.0, float("inf")):
+    env = os.environ.get("VBN_GIBBS_DAG_BUDGET")            # ablation: one per-wave budget
+    for budget in ((float(env),) if env else (0.8, 1.0, 1.2, 1.4, 2.0, 3.0, float("inf"))):
         done, phases, t = set(), [], 0.0
         while len(done) < len(deps):
             ready = sorted((i for i in deps if i not in done and deps[i] <= done), key=lambda i: (-cp[i], i))
