@@ -133,6 +133,54 @@ def _cases(name):
     return model_from_checkpoint(fx["model"]), fx["cases"]
 
 
+def _schedule_violations(rows, ic, phases):
+    """Ordering constraints a phased schedule breaks, restated independently of
+    plan.gibbs_step_deps: inside an update the LATENT step comes first and the SELECT last; for
+    updates h < g (sweep order) a step of g reading a slot h writes runs after h's SELECT, and a
+    step of h reading a slot g writes runs before g's LATENT.  "a before b" = an earlier phase,
+    or the same wave earlier in the same phase."""
+    pos = {op[1]: (k, w, j) for k, ph in enumerate(phases) for w, wops in enumerate(ph) for j, op in enumerate(wops)}
+
+    def before(a, b):
+        (ka, wa, ja), (kb, wb, jb) = pos[a], pos[b]
+        return ka < kb or (ka == kb and wa == wb and ja < jb)
+
+    def reads(i):
+        return set() if rows[i][P.S_ROLE] == P.ROLE_SELECT else set(_group_rw(rows, ic, i, i + 1)[0])
+
+    bad = []
+    groups, _, _ = P._gibbs_update_levels(rows, ic)
+    for g, (b, e) in enumerate(groups):
+        bad += [(b, i) for i in range(b + 1, e) if not before(b, i)]
+        bad += [(i, e - 1) for i in range(b, e - 1) if not before(i, e - 1)]
+        wg = _group_rw(rows, ic, b, e)[1]
+        for bh, eh in groups[:g]:
+            wh = _group_rw(rows, ic, bh, eh)[1]
+            bad += [(eh - 1, i) for i in range(b, e) if reads(i) & wh and not before(eh - 1, i)]
+            bad += [(i, b) for i in range(bh, eh) if reads(i) & wg and not before(i, b)]
+    return bad
+
+
+def test_schedule_checker_catches_reordering():
+    """_schedule_violations flags a step moved ahead of what it depends on (so the phase tests
+    above cannot pass vacuously)."""
+    model, cases = _cases("cfg2")
+    pk = P.PackedModel(model, torch.device("cpu"))
+    q = cases[0]["query"]
+    gp = P.build_gibbs_plan(pk, latent=[n for n in model.topo if n not in q["evidence"]],
+                            fixed=[n for n in model.topo if n in q["evidence"]], target=q["target"])
+    rows, ic, _ = gp.steps._vbn_host
+    phases, _ = P.gibbs_schedule(rows, ic, 4, split="dag")
+    assert _schedule_violations(rows, ic, phases) == []
+    # move the last phase's first op into phase 0: it depends on something later
+    k = max(k for k, ph in enumerate(phases) if any(ph) and any(op[0] != "run" for ops in ph for op in ops))
+    w = next(w for w, ops in enumerate(phases[k]) if ops)
+    moved = [[list(ops) for ops in ph] for ph in phases]
+    op = moved[k][w].pop(0)
+    moved[0][0].insert(0, op)
+    assert _schedule_violations(rows, ic, moved)
+
+
 @pytest.mark.parametrize("name", NAMES + ["cfg2"])
 @pytest.mark.parametrize("n_waves", [1, 2, 4])
 @pytest.mark.parametrize("split", [None, True, "dag"])
@@ -157,28 +205,9 @@ def test_gibbs_schedule_phases(name, n_waves, split):
         ops = [(k, w, op) for k, ph in enumerate(phases) for w, wops in enumerate(ph) for op in wops]
         assert sorted(op[1] for _, _, op in ops) == list(range(len(rows)))   # each step once
         phase_of = {op[1]: k for k, _, op in ops}
-        pos = {op[1]: (k, w, j) for k, ph in enumerate(phases) for w, wops in enumerate(ph)
-               for j, op in enumerate(wops)}
-
-        def before(a, b):
-            (ka, wa, ja), (kb, wb, jb) = pos[a], pos[b]
-            return ka < kb or (ka == kb and wa == wb and ja < jb)
-
+        assert _schedule_violations(rows, ic, phases) == []
         groups, level, _ = P._gibbs_update_levels(rows, ic)
-        # independent restatement of the constraints: per update pair h < g, through the slots
-        for g, (b, e) in enumerate(groups):
-            assert all(before(b, i) for i in range(b + 1, e)) and all(before(i, e - 1) for i in range(b, e - 1))
-            rd_g = [set(_group_rw(rows, ic, i, i + 1)[0]) if rows[i][P.S_ROLE] != P.ROLE_SELECT else set()
-                    for i in range(b, e)]
-            wg = _group_rw(rows, ic, b, e)[1]
-            for bh, eh in groups[:g]:
-                wh = _group_rw(rows, ic, bh, eh)[1]
-                for k, i in enumerate(range(b, e)):
-                    if rd_g[k] & wh:
-                        assert before(eh - 1, i), (i, eh - 1)
-                for i in range(bh, eh):
-                    if rows[i][P.S_ROLE] != P.ROLE_SELECT and _group_rw(rows, ic, i, i + 1)[0] & wg:
-                        assert before(i, b), (i, b)
+        for b, e in groups:
             assert P.gibbs_step_deps(rows, ic)[e - 1] >= set(range(b, e - 1))
         if split is True:                                   # the level form keeps the levels
             for (b, e), lv in zip(groups, level):
