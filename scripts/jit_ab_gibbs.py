@@ -58,8 +58,9 @@ def main():
     # kind set of this launch
     cap = {}
 
-    def capture(steps, in_cols, kind_set, dev, key):
+    def capture(steps, in_cols, kind_set, dev, key, *rest, **kw):
         cap["km"] = kind_set
+        cap["cw"] = rest[0] if rest else kw.get("chain_waves", 0)
         return None
     J.module_for = capture
     launch(1, 2)
@@ -72,6 +73,8 @@ def main():
         h = ctypes.c_void_p()
         buf = ctypes.create_string_buffer(code, len(code))
         _lib.check(lib.vbn_hip_module_load(buf, b"vbn_walk_plan", km, gp.n_steps, ctypes.byref(h)), "load")
+        if cap["cw"] > 0:                                   # chain workgroups (jit_variants --gibbs)
+            _lib.check(lib.vbn_hip_module_chain_waves(h, cap["cw"]), "chain waves")
         mods[path] = h.value
     ref = launch(7, 0)
     torch.cuda.synchronize()
@@ -93,7 +96,7 @@ def main():
         current["h"] = mods.get(v)
         out = launch(7, 0 if v == "interp" else 2)
         torch.cuda.synchronize()
-        print(json.dumps({"variant": os.path.basename(v), "kind_set": km, "sweep_ms": round(statistics.median(res[v]), 2),
+        print(json.dumps({"variant": os.path.basename(v), "kind_set": km, "chain_waves": cap["cw"], "sweep_ms": round(statistics.median(res[v]), 2),
                           "all_ms": [round(t, 2) for t in res[v]], "bit_identical": bool(torch.equal(out, ref)),
                           "specialised_flag": ops.LAST_WALK["specialised"]}), flush=True)
     J.module_for = orig

@@ -68,14 +68,19 @@ def gibbs_variants(variants):
     gp = build_gibbs_plan(pk, latent=[x for x in model.topo if x not in vals],
                           fixed=[x for x in model.topo if x in vals], target=target)
     steps, ic, _ = gp.steps._vbn_host
-    km = gp.kind_mask | 64 | 256            # half-wave, no injected draws (4096 chains)
-    src = jit.plan_source(steps, ic, km)
+    # the production form at 4096 chains (ops.gibbs_walk auto): full wave, no injected draws,
+    # chain workgroups of ops.CHAIN_WAVES waves on the cost model's schedule
+    from vectorizedbayesiannetwork_amd import ops
+    from vectorizedbayesiannetwork_amd.plan import gibbs_schedule
+    km = gp.kind_mask | 256
+    src = jit.plan_source(steps, ic, km, gibbs_schedule(steps, ic, ops.CHAIN_WAVES))
     base = jit.OPTIONS
     for v in variants:
         name, _, opts = v.partition("=")
         jit.OPTIONS = tuple(base) + tuple(opts.split())
         t0 = time.perf_counter()
         code = jit.compile_source(src)
+        os.makedirs(os.path.join(REPO, "exp"), exist_ok=True)
         out = os.path.join(REPO, "exp", f"gibbs_{name}.hsaco")
         with open(out, "wb") as f:
             f.write(code)
