@@ -43,7 +43,8 @@ import torch
 
 from . import ops
 from .model import BNModel, model_from_vbn
-from .plan import (KIND_ID, MODE_MCM, MODE_SAMPLE, MODE_WEIGHTED, GibbsPlan, PackedModel, QueryPlan, barren_pruned,
+from .plan import (F_PRE_OUT, KIND_ID, MODE_MCM, MODE_SAMPLE, MODE_WEIGHTED, S_FLAGS, S_KIND, GibbsPlan, PackedModel,
+                   QueryPlan, barren_pruned,
                    liveness_order, precompute_plans,
                    build_gibbs_plan, build_plan)
 from .registry import register_inference, register_sampling
@@ -308,9 +309,23 @@ def _query_rows(pq: torch.Tensor, b: int, steps: torch.Tensor) -> torch.Tensor:
     return pq.view(b, 64, w)[:, 0].contiguous()
 
 
-# the per-sample pre-pass on a side stream next to the per-query one (env VBN_PRE_STREAM=1: on).
-# Off: measured 2-3 % slower walks on cfg2 / anchor64 (profiles/r04_bench/r04j_ab_*)
-PRE_SIDE_STREAM = os.environ.get("VBN_PRE_STREAM", "0") == "1"
+# the per-sample pre-pass on a side stream next to the per-query one: on when the per-sample
+# pre-pass has KDE nodes (a few waves streaming whole point packs, latency-bound: cfg4 0.3 %
+# shorter steps, profiles/r05_bench/r05ae_*), off for NN-only ones (cfg2 / anchor64 2-3 % slower
+# steps, profiles/r04_bench/r04j_ab_*); env VBN_PRE_STREAM=1 / 0 forces it on / off
+PRE_SIDE_STREAM = {"1": True, "0": False}.get(os.environ.get("VBN_PRE_STREAM", ""))
+
+
+def _pre_side(plan) -> bool:
+    if PRE_SIDE_STREAM is not None:
+        return PRE_SIDE_STREAM
+    v = getattr(plan, "_pre_has_kde", None)
+    if v is None:
+        host = getattr(plan.pre.steps, "_vbn_host", None)
+        rows = host[0] if host is not None else plan.pre.steps.cpu().numpy()
+        v = bool(((rows[:, S_KIND] == KIND_ID["kde"]) & ((rows[:, S_FLAGS] & F_PRE_OUT) != 0)).any())
+        plan._pre_has_kde = v
+    return v
 _SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
 
 
@@ -372,7 +387,7 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
         # main walk
         # with both, the per-sample one (a few waves walking the root nodes, latency-bound) runs
         # on a side stream next to the per-query one
-        side = (_side_stream(pk.device) if (PRE_SIDE_STREAM and plan.pre is not None and plan.pre_q is not None)
+        side = (_side_stream(pk.device) if (plan.pre is not None and plan.pre_q is not None and _pre_side(plan))
                 else None)
         if side is not None:
             main = torch.cuda.current_stream(pk.device)
