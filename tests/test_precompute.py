@@ -127,3 +127,24 @@ def test_is_has_no_per_sample_precompute():
     model, pk, plan, vals = _plan("cfg2", "is")                 # IS: per-query root draws
     pc, pre, pre_q = P.precompute_plans(pk, plan)
     assert pre is None and pre_q is not None
+
+
+def test_side_stream_only_for_kde_per_sample_prepasses(monkeypatch):
+    """engines._pre_side: the per-sample pre-pass goes on a side stream when it has KDE nodes
+    (cfg4 / cfg5: long, latency-bound) and stays on the main stream for NN-only ones (cfg2 /
+    anchor64); VBN_PRE_STREAM forces either way."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import precompile_plans as PP
+    from vectorizedbayesiannetwork_amd import engines as E
+    want = {"cfg2": False, "anchor64": False, "cfg4": True, "cfg5": True}
+    for cfg, side in want.items():
+        plan = PP.plans_for(cfg)[1][0][1]
+        assert plan.pre is not None and plan.pre_q is not None
+        monkeypatch.setattr(E, "PRE_SIDE_STREAM", None)
+        plan.__dict__.pop("_pre_has_kde", None)
+        assert E._pre_side(plan) == side, cfg
+        for forced in (True, False):
+            monkeypatch.setattr(E, "PRE_SIDE_STREAM", forced)
+            assert E._pre_side(plan) == forced
