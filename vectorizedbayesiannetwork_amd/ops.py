@@ -259,8 +259,7 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
     ``plan_jit`` as for :func:`walk` (0 interpreter, 1 auto, 2 always specialised).
     ``chain_waves`` (specialised sweeps only): 1..8 = chain workgroups of that many waves that
     split each sweep's node updates by level (plan.gibbs_schedule; bit-identical chains), 0 = one
-    wave per chain group, -1 = auto (chain workgroups of CHAIN_WAVES when the one-wave form would
-    leave fewer than 2 waves per SIMD, CHAIN_WAVES_BELOW)."""
+    wave per chain group, -1 = auto (chain workgroups of auto_chain_waves(groups) waves)."""
     if wave_particles not in (0, 32, 64):
         raise ValueError(f"vbn_hip::gibbs_walk: wave_particles must be 0 (auto), 32 or 64, got {wave_particles}")
     if not -1 <= chain_waves <= 8:
@@ -324,7 +323,7 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
     auto_wp = wave_particles == 0
     if auto_wp:       # full waves wherever a chain workgroup may run (r05k: 4096 chains, 64 x 8 waves
         # 101.6 ms, 32 x 4 117.0 ms); the one-wave forms keep half waves for small batches
-        cw_auto = chain_waves if chain_waves >= 0 else (CHAIN_WAVES if total // WAVE < CHAIN_WAVES_BELOW else 0)
+        cw_auto = chain_waves if chain_waves >= 0 else auto_chain_waves(total // WAVE)
         wave_particles = 64 if cw_auto > 0 or total >= HALF_WAVE_BELOW else 32
     a.wave_particles = int(wave_particles)
     lib = _lib.load()
@@ -332,7 +331,7 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
         stream = ctypes.c_void_p(_stream_handle(device))
         cw = chain_waves
         if cw < 0:
-            cw = CHAIN_WAVES if total // wave_particles < CHAIN_WAVES_BELOW else 0
+            cw = auto_chain_waves(total // wave_particles)
         module = _plan_module(lib, a, steps, 0, int(steps.shape[0]), total * iters, plan_jit, device, cw)
         if module is None and auto_wp and total < HALF_WAVE_BELOW:
             a.wave_particles = 32                   # interpreter: half waves below HALF_WAVE_BELOW
@@ -346,11 +345,24 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
     return x
 
 
-# Gibbs launches whose one-wave form has fewer waves than this (2 per SIMD on 1024 SIMDs) run
-# the specialised sweep on chain workgroups of CHAIN_WAVES waves (r05k, 4096 chains: 8 waves
-# 101.6 ms, 4 waves 108.3 ms, full waves both)
-CHAIN_WAVES_BELOW = 2048
-CHAIN_WAVES = 8
+# Specialised Gibbs sweeps run on chain workgroups (plan.gibbs_schedule) at every batch size:
+# about CHAIN_TARGET_WAVES waves in all (4 per SIMD), so more chains take fewer waves per chain
+# group.  Sweep kernel ms, full wave, YAML defaults (profiles/r05_bench/r05ag_*, r05ah_*, r05w_*):
+#   2048 chains: 8 waves 73.0, 4: 97.8      4096: 8 94.7, 4 110.7
+#   8192: 4 157.4, 8 188.5, one-wave 318.9   16384: 2 287.6, 4 306.3, one-wave 335.3, 8 371.9
+#   32768: 2 562.2, 1 568.8, 4 595.1, one-wave 625.0
+CHAIN_TARGET_WAVES = 4096
+CHAIN_WAVES = 8               # the most (vbn_hip_module_chain_waves); 4096 chains -- the bench
+
+
+def auto_chain_waves(groups: int) -> int:
+    """Waves per chain workgroup for ``groups`` chain groups (64 -- half wave: 32 -- candidate
+    lanes each): the power of two nearest below CHAIN_TARGET_WAVES / groups, within [2, 8]."""
+    w = CHAIN_TARGET_WAVES // max(int(groups), 1)
+    cw = 2
+    while cw * 2 <= min(w, CHAIN_WAVES):
+        cw *= 2
+    return cw
 # below this many candidate lanes (B x 8) the one-wave sweep forms run half-wave (4 chains per
 # wave64): 1536 full waves = 1.5 per SIMD
 HALF_WAVE_BELOW = 1536 * 64
