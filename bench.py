@@ -109,17 +109,18 @@ def executed_work(model, plan, B: int, S: int, precomputed: bool):
     once per particle (plan.precompute_plans)."""
     if not precomputed or plan.pc is None:
         f, h = mlp_flops_per_particle(model, plan)
-        return f * B * S, h * B * S, kde_exps_per_particle(model, plan) * B * S
+        return f * B * S, h * B * S, kde_exps_per_particle(model, plan, executed=True) * B * S
     f32 = hid = exps = 0.0
     rows = plan.pc.steps.cpu().tolist()
     for i, row in enumerate(rows):
         one = _RowPlan([row])
         f, h = mlp_flops_per_particle(model, one)
-        e = kde_exps_per_particle(model, one)
+        e = kde_exps_per_particle(model, one, executed=True)
         fl = row[2]
         if fl & 8192:                                 # precomputed: pre-pass particles only
             n = B * 64 if fl & 32768 else S
-            kde_p1 = float(row[9]) if row[0] == KIND_ID["kde"] and row[1] == 1 else 0.0
+            kde_p1 = (float(row[9]) if row[0] == KIND_ID["kde"] and row[1] == 1 and row[31] < 0
+                      else 0.0)
             f32, hid, exps = f32 + f * n, hid + h * n, exps + kde_p1 * n + (e - kde_p1) * B * S
         else:
             f32, hid, exps = f32 + f * B * S, hid + h * B * S, exps + e * B * S
@@ -134,17 +135,20 @@ class _RowPlan:
         self.n_steps = len(rows)
 
 
-def kde_exps_per_particle(model, plan) -> float:
+def kde_exps_per_particle(model, plan, executed: bool = False) -> float:
     """Algorithmic kernel-weight evaluations (one exp each) of one particle in one walk:
     M for a sampled non-root KDE node (the CDF pass; the chunk rescan is not counted),
-    2M for a non-root log-prob (LSE over K_p and over K_p K_y), M for a root log-prob."""
+    2M for a non-root log-prob (LSE over K_p and over K_p K_y), M for a root log-prob.
+    ``executed``: without the CDF pass of nodes whose pass 1 comes from a moment table
+    (plan.kde_moment_table: no exps; a wave with a particle off the table's grid falls back to
+    the exp pass, which on-manifold workloads do not do)."""
     exps = 0.0
     for i in range(plan.n_steps):
         row = plan.steps[i].tolist()
         if row[0] != KIND_ID["kde"] or row[1] == 0:
             continue
         m, root = row[9], bool(row[2] & 2)
-        if row[1] == 1 and not root:
+        if row[1] == 1 and not root and not (executed and row[31] >= 0):
             exps += m
         if row[2] & 1:
             exps += m if root else 2 * m
@@ -233,6 +237,90 @@ KT_UNTIMED, KT_TIMED = 64, 20     # roofline kernel timing: untimed launches, th
 _T0 = time.perf_counter()
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``bench.py --gpus N`` started without a launcher: run N rank processes on this node as
+    fresh children (``torch.distributed.run``, rendezvous on 127.0.0.1) and return their exit
+    code.  This process has not touched the GPU (the package import does not) and is never
+    replaced by another program; rank 0's JSON line reaches stdout through the child."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def init_ranks(args):
+    """(world, rank, local, device) of this process; the process group when world > 1.
+    Exits non-zero when the launcher's WORLD_SIZE disagrees with ``--gpus``."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: launch with --nproc-per-node "
+              f"{args.gpus}, or run `python bench.py --gpus {args.gpus}` without a launcher", file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub:                                     # CPU rehearsal of the launch path only
+        if world > 1:
+            import torch.distributed as tdist
+            tdist.init_process_group("gloo")
+        return world, rank, local, "cpu"
+    if world > 1:
+        import torch.distributed as tdist
+        if args.dist_backend == "nccl":
+            if torch.cuda.device_count() < world:
+                print(f"bench.py: {world} ranks over RCCL need {world} GPUs, "
+                      f"{torch.cuda.device_count()} visible (--dist-backend gloo rehearses several "
+                      f"ranks on one GPU)", file=sys.stderr)
+                sys.exit(2)
+            torch.cuda.set_device(local)
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:                                         # rehearsal: ranks share the visible GPUs
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            tdist.init_process_group(args.dist_backend)
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local, f"cuda:{local}"
+
+
+def ranks_seen(world: int, backend: str, device) -> list:
+    """Every rank's global rank as the process group sees it (an all-gather), so the JSON line
+    proves that N ranks took part."""
+    if world == 1:
+        return [0]
+    import torch.distributed as tdist
+    dev = device if backend == "nccl" else "cpu"
+    mine = torch.tensor([tdist.get_rank()], dtype=torch.int64, device=dev)
+    outs = [torch.zeros_like(mine) for _ in range(tdist.get_world_size())]
+    tdist.all_gather(outs, mine)
+    return sorted(int(t.item()) for t in outs)
+
+
+def stub_main(args) -> None:
+    """``--stub``: the launch / rank / reporting path with no GPU work (CPU tests)."""
+    world, rank, local, device = init_ranks(args)
+    seen = ranks_seen(world, "gloo", device)
+    n_gpus = world
+    if world > 1:
+        import torch.distributed as tdist
+        n_gpus = tdist.get_world_size()
+    if rank == 0:
+        print(json.dumps({"metric": "stub", "value": 0.0, "unit": "queries/s", "n_gpus": n_gpus,
+                          "ranks_seen": seen, "steps": args.steps, "warmup": args.warmup,
+                          "stub": True}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
 def log(msg: str) -> None:
     """progress on stderr (the JSON line is the only stdout output)"""
     print(f"[bench {time.perf_counter() - _T0:7.1f}s rank {os.environ.get('RANK', '0')}] {msg}",
@@ -262,31 +350,33 @@ def main():
     ap.add_argument("--plan-jit", choices=("auto", "on", "off"), default="auto",
                     help="plan-specialised walk kernel (hiprtc, vectorizedbayesiannetwork_amd/jit.py) or the "
                          "step-table interpreter")
+    ap.add_argument("--stub", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
     if args.no_precompute:
         from vectorizedbayesiannetwork_amd import engines as _E
         _E.PRECOMPUTE = False
     if args.cpu_baseline_child:                       # fresh process, never touches the GPU
         cpu_baseline_child(args.config, args.cpu_queries, args.cpu_reps)
         return
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start the N ranks as children (before anything touches the GPU)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.stub:
+        stub_main(args)
+        return
 
     from vectorizedbayesiannetwork_amd.distributed import ShardedEngine
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local, device = init_ranks(args)
     dist = world > 1
     if dist:
         import torch.distributed as tdist
-        if args.dist_backend == "nccl":
-            torch.cuda.set_device(local)
-            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:                                         # rehearsal: ranks share the visible GPUs
-            local = local % max(1, torch.cuda.device_count())
-            torch.cuda.set_device(local)
-            tdist.init_process_group(args.dist_backend)
-    else:
-        torch.cuda.set_device(0)
-    device = f"cuda:{local}"
+        if tdist.get_world_size() != args.gpus:
+            print(f"bench.py: process group has {tdist.get_world_size()} ranks, --gpus {args.gpus}",
+                  file=sys.stderr)
+            sys.exit(2)
+    seen = ranks_seen(world, args.dist_backend, device)
 
     log(f"world {world}, backend {args.dist_backend if dist else '-'}, device {device}: building {args.config}")
     cfg, model, vbn, query = build_workload(args.config, device, world)
@@ -299,7 +389,9 @@ def main():
     gather = not args.no_gather
     # every N the same path: shard the global batch, gather pdf / samples on rank 0 (async,
     # overlapping the next step's walk); N = 1 is the trivial shard with no collective
-    sharded = ShardedEngine(engine, gather=gather, overlap=True)
+    # verify: every untimed call first checks that all ranks issue the same call (a 32-byte
+    # all-gather); off for the timed steps and the gather accounting
+    sharded = ShardedEngine(engine, gather=gather, overlap=True, verify=dist)
     vbn._inference = sharded
 
     def barrier():
@@ -392,6 +484,7 @@ def main():
     # gc.collect() here: a full collection right before t0 idles the GPU for long enough that
     # its clocks drop (0.976 vs 0.813 ms per step over the driver's 20 steps)
     log("timed region")
+    sharded.verify = False
     gc.disable()
     barrier()
     torch.cuda.synchronize()
@@ -490,7 +583,8 @@ def main():
         "metric": "posterior queries/sec (infer_posterior, n_samples=1024) at 1/2/4/8 MI355X",
         "value": round(value, 2),
         "unit": "queries/s",
-        "n_gpus": world,
+        "n_gpus": tdist.get_world_size() if dist else 1,
+        "ranks_seen": seen,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
@@ -507,7 +601,9 @@ def main():
                             else "step-table interpreter"),
                    "plan_compile_s": round(jit.STATS["compile_s"], 2), "plan_cache_hits": jit.STATS["disk_hits"],
                    "first_call_s": round(t_first, 2), "background_compile_wait_s": round(t_wait, 2),
-                   "precompute_nodes": {"per_sample": n_pre_s, "per_query": n_pre_q}},
+                   "precompute_nodes": {"per_sample": n_pre_s, "per_query": n_pre_q},
+                   "kde_moment_nodes": int(sum(1 for r in plan.steps.tolist()
+                                               if r[0] == KIND_ID["kde"] and r[1] == 1 and r[31] >= 0))},
         "roofline": roof,
     }
     if fallbacks:

@@ -10,8 +10,9 @@ count time ``infer_posterior`` on the same synthetic model and queries:
 * ``port``: the oracle's restatement with the reference's torch RNG calls (bench.py
   ``cpu_baseline_child``).
 
-One warm-up, median of 5 (1 for slow configs); prints port/ref time ratios (BASELINE.md
-requires 0.8-1.25).  Usage: python scripts/calibrate_cpu_baseline.py [cfg2 cfg3 anchor64]
+One warm-up, median of 5 (3 for the KDE configs cfg4 / cfg5, bench.py's reps); prints port/ref
+time ratios (BASELINE.md requires 0.8-1.25).
+Usage: python scripts/calibrate_cpu_baseline.py [--out FILE] [cfg2 cfg3 anchor64 cfg4 cfg5]
 """
 from __future__ import annotations
 
@@ -25,7 +26,9 @@ import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.environ.get("VBN_REFERENCE", "/root/reference")
-QUERIES = {"cfg2": 1024, "anchor64": 1024, "cfg3": 64}
+# queries per timed call (bench.py's bounded samples: KDE configs one call of ~5-17 s)
+QUERIES = {"cfg2": 1024, "anchor64": 1024, "cfg3": 64, "cfg4": 1, "cfg5": 4}
+REPS = {"cfg4": 3, "cfg5": 3}
 
 
 def child(impl: str, cfg_name: str, n_queries: int, reps: int) -> None:
@@ -80,12 +83,17 @@ def main(argv):
     sys.path.insert(0, REPO)
     import bench
     env = dict(os.environ, **bench.CPU_ENV)
+    args = argv[1:]
+    out_path = None
+    if args[:1] == ["--out"]:
+        out_path, args = args[1], args[2:]
     out = {}
-    for cfg_name in argv[1:] or ["cfg2", "cfg3", "anchor64"]:
+    for cfg_name in args or ["cfg2", "cfg3", "anchor64", "cfg4", "cfg5"]:
         nq = QUERIES[cfg_name]
         res = {}
         for impl in ("ref", "port"):
-            r = subprocess.run([sys.executable, __file__, "--child", impl, cfg_name, str(nq), "5"], env=env,
+            r = subprocess.run([sys.executable, __file__, "--child", impl, cfg_name, str(nq),
+                                str(REPS.get(cfg_name, 5))], env=env,
                                capture_output=True, text=True, timeout=3600)
             if r.returncode != 0:
                 raise RuntimeError(r.stderr[-3000:])
@@ -93,7 +101,16 @@ def main(argv):
         ratio = res["port"]["median_s"] / res["ref"]["median_s"]
         out[cfg_name] = {"queries": nq, "ref_qps": nq / res["ref"]["median_s"], "port_qps": nq / res["port"]["median_s"],
                          "port_over_ref_time": ratio, "threads": res["ref"]["threads"]}
+        out[cfg_name]["ref_times_s"] = res["ref"]["times"]
+        out[cfg_name]["port_times_s"] = res["port"]["times"]
         print(json.dumps({cfg_name: out[cfg_name]}), flush=True)
+    if out_path:
+        with open(out_path, "w") as f:
+            json.dump({"what": "scripts/calibrate_cpu_baseline.py in the build container (8 cores, "
+                               "MALLOC_MMAP_MAX_=0 MALLOC_TRIM_THRESHOLD_=1e12, no_grad, fresh process "
+                               "each, 1 warm-up + median): the reference's own infer_posterior (VBN.load "
+                               "of our VBN.save checkpoint) vs the oracle port bench.py times on the GPU box",
+                       **out}, f, indent=1)
     return 0
 
 

@@ -256,3 +256,39 @@ def test_gloo_sharded_engine_keeps_a_seeded_engines_sequence():
     assert outs1 == [] and max(pending1) <= 2, pending1           # one call (pdf + samples) in flight
     shard = 4 * S * 4 + 4 * S * 1 * 4                 # pdf [4, S] + samples [4, S, 1] fp32 from rank 1
     assert nbytes == calls * shard
+
+
+def _verify_worker(rank, world, init, out_q):
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
+    try:
+        eng = ShardedEngine(StubEngine(), gather=True, verify=True)
+        ev = torch.linspace(-1, 1, 8).unsqueeze(1)
+        pdf, _ = eng.infer_posterior(None, Query(target="y", evidence={"x": ev}, do={}))
+        ok = pdf is not None or rank != 0
+        # the second call diverges: rank 1 queries another target (a different plan, and in a
+        # real engine possibly another collective sequence) -- every rank must refuse it
+        try:
+            eng.infer_posterior(None, Query(target="y" if rank == 0 else "z", evidence={"x": ev}, do={}))
+            err = None
+        except RuntimeError as e:
+            err = str(e)
+        out_q.put((rank, ok, err))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_verify_refuses_diverging_calls():
+    """ShardedEngine(verify=True): a call some rank issues differently raises on every rank
+    (instead of a collective one rank never joins)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = _rendezvous()
+    procs = [ctx.Process(target=_verify_worker, args=(r, 2, init, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, err in res:
+        assert ok
+        assert err is not None and "disagree" in err, (rank, err)

@@ -296,3 +296,42 @@ def test_chain_sweep_source():
     assert "__launch_bounds__(4 * WAVE)" in src
     src8 = jit.plan_source(rows, ic, gp.kind_mask | 256, P.gibbs_schedule(rows, ic, 8))
     assert "#define VBN_PLAN_CHAIN_WAVES 8" in src8 and "__launch_bounds__(8 * WAVE)" in src8
+
+
+def _gibbs_plan_of(n_nodes, kinds=("linear_gaussian",)):
+    from vectorizedbayesiannetwork_amd import synthetic
+    from vectorizedbayesiannetwork_amd.model import random_init_model
+    g = synthetic.random_dag(n_nodes, seed=0)
+    data = synthetic.sem_data(g, 256, seed=0)
+    model = random_init_model(g, synthetic.round_robin_kinds(g, kinds), data, seed=0)
+    pk = P.PackedModel(model, torch.device("cpu"))
+    ev = set(model.topo[: n_nodes // 4])
+    gp = P.build_gibbs_plan(pk, latent=[n for n in model.topo if n not in ev],
+                            fixed=[n for n in model.topo if n in ev], target=model.topo[-1])
+    return gp
+
+
+def test_chain_waves_fit_lds():
+    """the auto chain-wave choice counts the sweep unit's static score rows
+    (vbn_lp_rows) as well as the dynamic slots + scratch rows, and falls back to fewer waves, then
+    the one-wave form, when a chain workgroup would not fit the CU's 160 KiB of LDS."""
+    from vectorizedbayesiannetwork_amd import jit, ops
+    small = _gibbs_plan_of(32)
+    init = small.init
+    rows, ic, key = small.steps._vbn_host
+    for cw in (1, 2, 4, 8):
+        _, n_rows = P.gibbs_schedule(rows, ic, cw)
+        want = (init.n_slots + cw * max(init.max_out, 1)) * 256 + max(n_rows, 1) * 256
+        assert jit.chain_lds_bytes(rows, ic, key, cw, init.n_slots, init.max_out) == want
+    assert ops.fit_chain_waves(small.steps, 8, init.n_slots, init.max_out) == 8
+    # a wide DAG: its score rows alone (one per LATENT / child step) exceed 160 KiB at 8 waves
+    wide = _gibbs_plan_of(700)
+    wi = wide.init
+    wrows, wic, wkey = wide.steps._vbn_host
+    assert jit.chain_lds_bytes(wrows, wic, wkey, 8, wi.n_slots, wi.max_out) > jit.LDS_BYTES
+    cw = ops.fit_chain_waves(wide.steps, 8, wi.n_slots, wi.max_out)
+    assert cw < 8
+    if cw > 0:
+        assert jit.chain_lds_bytes(wrows, wic, wkey, cw, wi.n_slots, wi.max_out) <= jit.LDS_BYTES
+    # steps without a host copy (no specialised unit) keep the requested count
+    assert ops.fit_chain_waves(torch.zeros(1, 32, dtype=torch.int32), 4, 10, 1) == 4

@@ -80,6 +80,11 @@ def _check(name, bad, draws, n_expect):
     unexplained = bad & ~ties
     print(f"{name}: {int(bad.sum())} differing particles of {bad.size}, "
           f"{int(ties.sum())} with a categorical near-tie (< {TIE}), {draws.n_categorical} categorical draws")
+    if bad.any():
+        mm = np.sort(draws.min_margin()[bad])
+        print(f"{name}: smallest categorical margins of the differing particles {mm[:8].tolist()}; "
+              f"particles with a margin < 1e-7 / 3e-7 / 1e-6: {int((draws.min_margin() < 1e-7).sum())} / "
+              f"{int((draws.min_margin() < 3e-7).sum())} / {int((draws.min_margin() < 1e-6).sum())}")
     assert bad.shape == (n_expect[0], n_expect[1])
     assert not unexplained.any(), (
         f"{name}: {int(unexplained.sum())} particles differ without a categorical near-tie "

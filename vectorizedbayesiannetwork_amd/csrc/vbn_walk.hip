@@ -525,6 +525,7 @@ struct vbn_plan_module {
   unsigned kmi;
   int n_steps;
   int chain_waves;     // > 0: a Gibbs sweep on chain workgroups (vbn_hip_module_chain_waves)
+  int static_lds;      // the kernel's static LDS (a sweep unit's vbn_lp_rows score rows), bytes
 };
 
 extern "C" int vbn_hip_module_load(const void* image, const char* kernel, uint32_t kind_set, int32_t n_steps,
@@ -538,8 +539,11 @@ extern "C" int vbn_hip_module_load(const void* image, const char* kernel, uint32
     delete m;
     return fail((int)e, hipGetErrorString(e));
   }
+  int st_lds = 0;
+  if (hipFuncGetAttribute(&st_lds, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, m->fn) != hipSuccess) st_lds = 0;
   m->kmi = kind_set;
   m->n_steps = n_steps;
+  m->static_lds = st_lds;
   *handle = m;
   return 0;
 }
@@ -583,7 +587,9 @@ extern "C" int vbn_hip_walk_module(const void* handle, const vbn_walk_args* a, v
     const int64_t wp = a->wave_particles == 32 ? 32 : WAVE;
     const int64_t rows = a->max_out > 0 ? a->max_out : 1;
     const int64_t lds = ((int64_t)a->n_slots + m->chain_waves * rows) * WAVE * (int64_t)sizeof(float);
-    if (lds > 160 * 1024) return fail(VBN_E_LDS, "vbn_hip_walk_module: chain workgroup needs more than 160 KiB of LDS");
+    // the dynamic slots + scratch rows and the unit's static score rows share the CU's 160 KiB
+    if (lds + m->static_lds > 160 * 1024)
+      return fail(VBN_E_LDS, "vbn_hip_walk_module: chain workgroup needs more than 160 KiB of LDS");
     const int64_t blocks = (a->n_queries * (int64_t)a->n_samples + wp - 1) / wp;
     if (blocks > 0x7fffffffLL) return fail(VBN_E_ARGS, "vbn_hip_walk: too many particles for one launch");
     w.grid = dim3((unsigned)blocks);

@@ -42,6 +42,8 @@
 
 #define WAVE 64
 #define KDE_CHUNKS 16
+// kde steps: blob offset of the one-feature moment table (plan.kde_moment_table), -1 = none
+#define KDE_MT(st) ((st).reserved[7])
 #define KDE_REC_TAIL 16  // weight-0 record rows after the last point (plan.py KDE_REC_TAIL)
 #define LOG_2PI_F 1.8378770664093453f
 
@@ -1528,6 +1530,36 @@ __device__ __forceinline__ double kde_pass1(const bf16x8* __restrict__ pa, int c
   return tot;
 }
 
+// Pass 1 of a one-feature node from its moment table (plan.kde_moment_table, round 6): around
+// the grid centre u_g nearest u = 2 x', S_c(u) = sum_k d^k T[g][c][k] with d = u - u_g, where
+// T[g][c][k] = sum_{j in c} exp2(u_g y'_j - |y'_j|^2) (ln2 y'_j)^k / k! (float64 sums, host).
+// The series' remainder is < 3e-8 of every weight (KDE_MT_Z), so the chunk sums equal the
+// exp-by-exp sums to f32 rounding -- and cost KDE_MT_TERMS - 1 FMAs and one 16-byte load per
+// chunk instead of one v_exp_f32 and half a v_pk_add_f32 per point.  The factored form (shift
+// 0): the caller takes this path only when every lane has fform.  Returns false (the wave then
+// runs the MFMA pass) when some lane's u lies outside the grid (or is NaN).
+// Table: header [u_lo, 1 / delta, delta, n_cells (int32 bits)], rows [n_cells][KDE_CHUNKS][4].
+__device__ __forceinline__ bool kde_pass1_moments(const float* __restrict__ T, float u, const Lane& L,
+                                                  double& tot) {
+  const cfloat* H = CP(T);
+  const float u_lo = H[0], inv_d = H[1], dlt = H[2];
+  const float n_cells = (float)__float_as_int(H[3]);
+  const float gr = rintf((u - u_lo) * inv_d);           // nearest centre (NaN u: not in range)
+  const bool in = gr >= 0.f && gr < n_cells;
+  if (!__all(in)) return false;
+  const float d = u - fmaf(gr, dlt, u_lo);              // the centre exactly as the host formed it
+  const float4* __restrict__ row = reinterpret_cast<const float4*>(T + 4) + (int)gr * KDE_CHUNKS;
+  tot = 0.0;
+#pragma unroll
+  for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
+    const float4 c = row[ch];
+    const float cs = fmaf(fmaf(fmaf(c.w, d, c.z), d, c.y), d, c.x);
+    L.scr[ch * WAVE + L.lane] = cs;
+    tot += (double)cs;
+  }
+  return true;
+}
+
 // Sum over all nb32 blocks of a log-density pack (kde_logp_mfma)
 template <int KG, int PG>
 __device__ __forceinline__ float kde_sum_all(const bf16x8* __restrict__ pa, int nb32, const Lane& L,
@@ -1652,7 +1684,10 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
     const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
     const bool fform = __all(-negsq <= KDE_FFORM_MAX);
     shift = fform ? 0.f : -negsq;
-    if (nf == 1)
+    // one-feature nodes with a moment table: pass 1 from the table (kde_pass1_moments)
+    const bool mom = nf == 1 && fform && KDE_MT(st) >= 0 && kde_pass1_moments(L.P + KDE_MT(st), 2.f * xv[0], L, tot);
+    if (mom) {
+    } else if (nf == 1)
       tot = kde_pass1<1, 1>(pa, cb >> 1, L, slots, scl, nf, fform);
     else if (nf == 2 && fform)
       tot = kde_pass1<1, 2>(pa, cb >> 1, L, slots, scl, nf, fform);
@@ -1727,7 +1762,9 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
 __device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L, bool root, float c_p,
                                               float c_y, float cy, float log_n, float& lp) {
   const int M = st.k, dp = st.aux0, D = st.out_dim, lane = L.lane;
-  const int nb32 = (KDE_CHUNKS * kde_cb(M)) >> 1;
+  // the blocks holding points (a whole number of KDE_PF blocks), not the chunk-padded pack: the
+  // blocks past them hold only weight-0 padding, whose +0 terms leave every sum unchanged
+  const int nb32 = min((KDE_CHUNKS * kde_cb(M)) >> 1, (((M + 31) >> 5) + KDE_PF - 1) / KDE_PF * KDE_PF);
   int slots[4] = {0, 0, 0, 0};
   float scl[4] = {c_p, c_p, c_p, c_p};
   for (int f = 0; f < dp; ++f) slots[f] = L.ic[st.in_off + f];

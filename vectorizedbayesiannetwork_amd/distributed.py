@@ -94,8 +94,13 @@ class ShardedEngine:
     """Wrap an engine (``infer_posterior`` or ``sample``) for query-sharded multi-GPU runs."""
 
     def __init__(self, engine, group=None, gather: bool = False, dst: int = 0, overlap: bool = False,
-                 force_collectives: bool = False):
+                 force_collectives: bool = False, verify: bool = False):
         self.engine = engine
+        # verify=True: before each call, all-gather (call index, method, batch size, target) and
+        # raise on any rank that disagrees -- ranks issuing different collective sequences would
+        # otherwise hang in a collective another rank never issues (one 32-byte all-gather per
+        # call; bench.py turns it on outside its timed region)
+        self.verify = bool(verify)
         # issue the seed broadcast, flag all-reduce and gathers even in a world of one rank (an
         # initialised process group of size 1: the RCCL code path on a one-GPU box, tests)
         self.force_collectives = bool(force_collectives)
@@ -205,14 +210,25 @@ class ShardedEngine:
             kw["_resample_u"] = [_slice_rows(u, 0, b0, b1, n_total) for u in kw["_resample_u"]]
         return kw
 
-    def _check(self, n_total: int, world: int) -> None:
+    def _check(self, n_total: int, world: int, method: int = 0, target=None) -> None:
         if n_total < world:
             raise ValueError(f"{n_total} queries cannot be sharded over {world} ranks")
+        if not self.verify or not dist.is_initialized() or (world == 1 and not self.force_collectives):
+            return
+        import zlib
+        tag = zlib.crc32(repr(target).encode()) & 0x7FFFFFFF
+        mine = torch.tensor([self._calls + 1, method, n_total, tag], dtype=torch.int64, device=self._device())
+        outs = [torch.empty_like(mine) for _ in range(dist.get_world_size(self.group))]
+        dist.all_gather(outs, mine, group=self.group)
+        rows = [tuple(int(v) for v in o.tolist()) for o in outs]
+        if any(r != rows[0] for r in rows):
+            raise RuntimeError("ShardedEngine: ranks disagree on the collective sequence "
+                               f"(call, method, n_queries, target tag) per rank: {rows}")
 
     def infer_posterior(self, vbn, query, **kwargs):
         rank, world = _world(self.group)
         n_total = infer_batch_size(query.evidence, getattr(query, "do", None))
-        self._check(n_total, world)
+        self._check(n_total, world, 1, query.target)
         self._calls += 1
         b0, b1 = shard_bounds(n_total, rank, world)
         self._set_base(b0)
@@ -228,7 +244,7 @@ class ShardedEngine:
     def sample(self, vbn, query, n_samples=None, **kwargs):
         rank, world = _world(self.group)
         n_total = infer_batch_size(query.evidence, getattr(query, "do", None))
-        self._check(n_total, world)
+        self._check(n_total, world, 2, query.target)
         self._calls += 1
         b0, b1 = shard_bounds(n_total, rank, world)
         self._set_base(b0)

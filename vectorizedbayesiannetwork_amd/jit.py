@@ -319,6 +319,37 @@ def wait_pending(timeout: Optional[float] = None) -> bool:
     return True
 
 
+def _split_env(chain_waves: int) -> str:
+    return os.environ.get("VBN_GIBBS_SPLIT", "") if chain_waves > 0 else ""
+
+
+def _split_arg(split_env: str):
+    # VBN_GIBBS_SPLIT=0/1/levels/dag: whole / split / per-level choice / the step-level schedule
+    # (ablation); unset: the cost model
+    return {"0": False, "1": True, "dag": "dag", "levels": "levels"}.get(split_env)
+
+
+LDS_BYTES = 160 * 1024         # per CU (one chain workgroup must fit)
+_chain_lds: dict = {}
+
+
+def chain_lds_bytes(steps: np.ndarray, in_cols: np.ndarray, plan_key: str, chain_waves: int, n_slots: int,
+                    max_out: int) -> int:
+    """LDS of one chain workgroup of ``chain_waves`` waves running this sweep table: the dynamic
+    slots + per-wave scratch rows (vbn_hip_walk_module) plus the unit's static score rows
+    (``vbn_lp_rows``, plan_source: n_rows of the schedule)."""
+    split_env = _split_env(chain_waves)
+    k = (plan_key, chain_waves, n_slots, max_out, split_env)
+    got = _chain_lds.get(k)
+    if got is None:
+        from .plan import gibbs_schedule
+        _, n_rows = gibbs_schedule(steps, in_cols, chain_waves, split=_split_arg(split_env))
+        rows = max_out if max_out > 0 else 1
+        got = (n_slots + chain_waves * rows) * 256 + max(int(n_rows), 1) * 256
+        _chain_lds[k] = got
+    return got
+
+
 def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_index: int,
                plan_key: str, chain_waves: int = 0, compile: str = "sync") -> Optional[int]:
     """Loaded module handle for (plan, kind set, device); None if the plan cannot be specialised
@@ -329,7 +360,7 @@ def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_ind
     ``chain_waves`` > 0: a Gibbs sweep table run on chain workgroups of that many waves
     (plan.gibbs_schedule)."""
     global _warned
-    split_env = os.environ.get("VBN_GIBBS_SPLIT", "") if chain_waves > 0 else ""
+    split_env = _split_env(chain_waves)
     mk = (device_index, f"{plan_key}:{kind_set}:{chain_waves}:{split_env}")
     h = _modules.get(mk)
     if h is not None:
@@ -344,10 +375,7 @@ def module_for(steps: np.ndarray, in_cols: np.ndarray, kind_set: int, device_ind
             schedule = None
             if chain_waves > 0:
                 from .plan import gibbs_schedule
-                # VBN_GIBBS_SPLIT=0/1/levels/dag: whole / split / per-level choice / the step-level schedule
-                # (ablation); unset: the cost model
-                split = {"0": False, "1": True, "dag": "dag", "levels": "levels"}.get(split_env)
-                schedule = gibbs_schedule(steps, in_cols, chain_waves, split=split)
+                schedule = gibbs_schedule(steps, in_cols, chain_waves, split=_split_arg(split_env))
             src = plan_source(steps, in_cols, kind_set, schedule)
             key = _source_key(src)
             code = _cached_code(key)

@@ -249,7 +249,7 @@ def _walk_fake(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samp
 def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: Optional[Tensor],
                state: Tensor, n_queries: int, n_slots: int, max_out: int, fixed_ld: int, noise_b: int,
                n_noise: int, dmax: int, out_dim: int, iters: int, burn_in: int, thin: int, q_base: int,
-               seed: int, offset: int, kind_mask: int, wbuf: int = 0, wave_particles: int = 64,
+               seed: int, offset: int, kind_mask: int, wbuf: int = 0, wave_particles: int = 0,
                plan_jit: int = 1, chain_waves: int = -1) -> Tensor:
     """``iters`` Gibbs sweeps (gibbs.py:34-87) over B chains x 8 candidate lanes, started from
     ``state`` [n_slots + 1, B*8]; returns the collected target values [B, n_collect, out_dim].
@@ -321,17 +321,17 @@ def gibbs_walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, no
     a.n_noise = n_noise
     a.wbuf_floats = int(wbuf)
     auto_wp = wave_particles == 0
+    cw = chain_waves
+    if cw < 0:        # auto: chain workgroups whose LDS fits (fit_chain_waves), else the one-wave form
+        cw = fit_chain_waves(steps, auto_chain_waves(total // (WAVE if auto_wp else wave_particles)),
+                             n_slots, max_out)
     if auto_wp:       # full waves wherever a chain workgroup may run (r05k: 4096 chains, 64 x 8 waves
         # 101.6 ms, 32 x 4 117.0 ms); the one-wave forms keep half waves for small batches
-        cw_auto = chain_waves if chain_waves >= 0 else auto_chain_waves(total // WAVE)
-        wave_particles = 64 if cw_auto > 0 or total >= HALF_WAVE_BELOW else 32
+        wave_particles = 64 if cw > 0 or total >= HALF_WAVE_BELOW else 32
     a.wave_particles = int(wave_particles)
     lib = _lib.load()
     with torch.cuda.device(device):
         stream = ctypes.c_void_p(_stream_handle(device))
-        cw = chain_waves
-        if cw < 0:
-            cw = auto_chain_waves(total // wave_particles)
         module = _plan_module(lib, a, steps, 0, int(steps.shape[0]), total * iters, plan_jit, device, cw)
         if module is None and auto_wp and total < HALF_WAVE_BELOW:
             a.wave_particles = 32                   # interpreter: half waves below HALF_WAVE_BELOW
@@ -363,6 +363,19 @@ def auto_chain_waves(groups: int) -> int:
     while cw * 2 <= min(w, CHAIN_WAVES):
         cw *= 2
     return cw
+def fit_chain_waves(steps, cw: int, n_slots: int, max_out: int) -> int:
+    """The largest wave count <= ``cw`` (8, 4, 2, 1) whose chain workgroup fits the CU's LDS
+    with the sweep unit's static score rows (jit.chain_lds_bytes); 0 (the one-wave form) when
+    none does.  Steps without a host copy (no specialised unit) keep ``cw``."""
+    host = getattr(steps, "_vbn_host", None)
+    if host is None or cw <= 0:
+        return cw
+    from . import jit
+    while cw > 0 and jit.chain_lds_bytes(host[0], host[1], host[2], cw, n_slots, max_out) > jit.LDS_BYTES:
+        cw //= 2
+    return cw
+
+
 # below this many candidate lanes (B x 8) the one-wave sweep forms run half-wave (4 chains per
 # wave64): 1536 full waves = 1.5 per SIMD
 HALF_WAVE_BELOW = 1536 * 64

@@ -191,6 +191,84 @@ def _kde_pack_valu(y: np.ndarray) -> np.ndarray:
     return a.reshape(-1, 8, nf).transpose(0, 2, 1)
 
 
+# ---- moment tables of one-feature KDE nodes (csrc kde_pass1_moments, round 6) ---------------
+# Pass 1 needs, per particle u = 2 x' and chunk c, S_c(u) = sum_{j in c} exp2(u y'_j - |y'_j|^2).
+# Around a grid centre u_g, exp2(u y') = exp2(u_g y') * exp(d ln2 y') with d = u - u_g, so
+#   S_c(u) = sum_k d^k T[g][c][k],   T[g][c][k] = sum_{j in c} exp2(u_g y'_j - |y'_j|^2) (ln2 y'_j)^k / k!
+# truncated after KDE_MT_TERMS terms: the remainder of each point's series is below
+# |z|^K / K! e^|z| with |z| = |d| ln2 |y'_j| <= KDE_MT_Z, i.e. a relative error < KDE_MT_EPS on
+# every weight, all of the same sign -- below the f32 rounding of a 640-term chunk sum.
+KDE_MOMENTS = os.environ.get("VBN_KDE_MOMENTS", "1") != "0"      # A/B: 0 = MFMA pass 1 for every node
+KDE_MT_TERMS = 4
+KDE_MT_Z = 0.028                 # |d| ln2 max|y'| at the cell edge: 0.028^4 / 24 * e^0.028 < 3e-8
+KDE_MT_MAX_CELLS = 16384         # table size bound (16384 x 16 x 4 floats = 4 MiB per node)
+KDE_MT_EXP_MAX = 100.0           # largest log2 weight a cell may hold (f32 sums stay finite)
+KDE_MT_EXP_MIN = -80.0           # every cell keeps a weight above 2^-80 (no all-underflow chunk set)
+KDE_MT_HEADER = 4                # floats: u_lo, 1 / delta, delta, n_cells (int32 bits)
+
+
+def kde_moment_cells(y: np.ndarray):
+    """Grid of one-feature KDE parent points y' (float32, scaled): (u_lo, delta, inv_delta,
+    n_cells) as float32 / int, the particle range u = 2 x' it covers being 2 [min y' - W,
+    max y' + W] with W = max(span, 2) (a particle outside it takes the MFMA pass); None when
+    the grid would exceed KDE_MT_MAX_CELLS or a cell's weights leave [2^-80, 2^100]."""
+    y = np.asarray(y, np.float32).reshape(-1)
+    y64 = y.astype(np.float64)
+    sq = (y64 * y64).astype(np.float32).astype(np.float64)        # |y'|^2 as the records hold it
+    ymax_abs = float(np.abs(y64).max())
+    span = float(y64.max() - y64.min())
+    w = max(span, 2.0)
+    lo, hi = 2.0 * (float(y64.min()) - w), 2.0 * (float(y64.max()) + w)
+    if ymax_abs == 0.0:
+        delta = hi - lo
+    else:
+        delta = 2.0 * KDE_MT_Z / (math.log(2.0) * ymax_abs)
+    delta32 = np.float32(delta)
+    lo32 = np.float32(lo)
+    n = int(math.ceil((hi - lo) / float(delta32))) + 1
+    if n > KDE_MT_MAX_CELLS:
+        return None
+    centres = kde_moment_centres(lo32, delta32, n)
+    # the largest log2 weight of each cell, u_g y' - |y'|^2 over the points (a max of lines in u)
+    e_max = np.max(centres[:, None] * y64[None, :] - sq[None, :], axis=1)
+    if e_max.max() > KDE_MT_EXP_MAX or e_max.min() < KDE_MT_EXP_MIN:
+        return None
+    return lo32, delta32, np.float32(1.0 / float(delta32)), n
+
+
+def kde_moment_centres(lo32, delta32, n: int) -> np.ndarray:
+    """Cell centres exactly as the kernel forms them: fmaf(g, delta, u_lo) in float32 (one
+    rounding of the exact g * delta + u_lo, which float64 holds for g < 2^14)."""
+    g = np.arange(n, dtype=np.float64)
+    return (g * np.float64(delta32) + np.float64(lo32)).astype(np.float32).astype(np.float64)
+
+
+def kde_moment_table(y: np.ndarray, m_chunk: int) -> Optional[np.ndarray]:
+    """The moment table of one-feature KDE parent points y' (float32, scaled) with chunks of
+    ``m_chunk`` points (the inverse-CDF chunks: _kde_cb(M) * 16): header [u_lo, 1 / delta,
+    delta, n_cells (int32 bits)] then [n_cells][KDE_CHUNKS][KDE_MT_TERMS] float32 (float64
+    sums, one rounding).  None when kde_moment_cells declines the node."""
+    cells = kde_moment_cells(y)
+    if cells is None:
+        return None
+    lo32, delta32, inv32, n = cells
+    y64 = np.asarray(y, np.float32).reshape(-1).astype(np.float64)
+    sq = (y64 * y64).astype(np.float32).astype(np.float64)
+    m = y64.size
+    centres = kde_moment_centres(lo32, delta32, n)
+    pw = np.stack([(math.log(2.0) * y64) ** k / math.factorial(k) for k in range(KDE_MT_TERMS)], axis=1)
+    tab = np.zeros((n, KDE_CHUNKS, KDE_MT_TERMS), np.float64)
+    for c in range(KDE_CHUNKS):
+        j0, j1 = min(m, c * m_chunk), min(m, (c + 1) * m_chunk)
+        if j0 >= j1:
+            continue
+        wts = np.exp2(centres[:, None] * y64[None, j0:j1] - sq[None, j0:j1])     # [n, pts]
+        tab[:, c, :] = wts @ pw[j0:j1]
+    head = np.array([lo32, inv32, delta32, 0], np.float32)
+    head[3:4] = np.array([n], np.int32).view(np.float32)
+    return np.concatenate([head, tab.astype(np.float32).reshape(-1)])
+
+
 def _np(t: torch.Tensor) -> np.ndarray:
     return t.detach().to("cpu", torch.float32).numpy()
 
@@ -392,6 +470,10 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
             offs["kq"] = blob.add(_kde_pack_b32(_np(pts_p) * c_p))
             offs["kr"] = blob.add(_kde_pack([_np(pts_p) * c_p], records=True))
             offs["kv"] = blob.add(_kde_pack_valu(_np(pts_p) * c_p))
+            if dp == 1 and KDE_MOMENTS:               # pass 1 from a moment table (kde_pass1_moments)
+                mt = kde_moment_table((_np(pts_p) * c_p).reshape(-1), _kde_cb(m) * 16)
+                if mt is not None:
+                    offs["kmt"] = blob.add(mt)
         if dp + D <= 4:
             feats = np.concatenate(([_np(pts_p).reshape(m, -1) * c_p] if dp else [])
                                    + [_np(pts_y).reshape(m, -1) * c_y], axis=1)
@@ -710,7 +792,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
             row[S_FLAGS] = fl
         row[S_OFF_KR] = npk.offs.get("kr", -1)
         row[S_OFF_KV] = npk.offs.get("kv", -1)
-        row[S_RES7] = -1
+        row[S_RES7] = npk.offs.get("kmt", -1)   # kde: moment table of a one-feature node
         if "wblk" in npk.offs and (n in latent_s or n in logp_s or n in params_s):
             row[S_WBLK_OFF] = npk.offs["wblk"]
             row[S_WBLK_LEN] = npk.offs["wblk_len"]
