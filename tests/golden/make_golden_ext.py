@@ -22,6 +22,12 @@ import argparse
 import os
 import sys
 
+# one OpenMP / MKL thread, fixed before torch loads: the reference's fits (linear_gaussian's
+# lstsq, the NN epochs) then reproduce bit for bit from run to run (under the default thread
+# pool the ridge weights drifted by up to 2.4e-7 between regenerations)
+os.environ["OMP_NUM_THREADS"] = "1"
+os.environ["MKL_NUM_THREADS"] = "1"
+
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -95,6 +101,7 @@ def main():
     os.environ.setdefault("CI", "1")
     import networkx as nx
     import vbn as vbn_mod  # noqa: F401
+    G.deterministic_fits()
     from vectorizedbayesiannetwork_amd import synthetic
 
     torch.manual_seed(0)

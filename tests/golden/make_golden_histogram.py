@@ -17,6 +17,12 @@ import argparse
 import os
 import sys
 
+# one OpenMP / MKL thread, fixed before torch loads: the reference's fits (linear_gaussian's
+# lstsq, the NN epochs) then reproduce bit for bit from run to run (under the default thread
+# pool the ridge weights drifted by up to 2.4e-7 between regenerations)
+os.environ["OMP_NUM_THREADS"] = "1"
+os.environ["MKL_NUM_THREADS"] = "1"
+
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))

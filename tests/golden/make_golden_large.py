@@ -22,6 +22,12 @@ import argparse
 import os
 import sys
 
+# one OpenMP / MKL thread, fixed before torch loads: the reference's fits (linear_gaussian's
+# lstsq, the NN epochs) then reproduce bit for bit from run to run (under the default thread
+# pool the ridge weights drifted by up to 2.4e-7 between regenerations)
+os.environ["OMP_NUM_THREADS"] = "1"
+os.environ["MKL_NUM_THREADS"] = "1"
+
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -94,6 +100,7 @@ def main():
     sys.path.insert(0, G.REF)
     os.environ.setdefault("CI", "1")
     import vbn as vbn_mod
+    G.deterministic_fits()
 
     torch.manual_seed(0)
     fixtures = {}

@@ -24,6 +24,12 @@ import argparse
 import os
 import sys
 
+# one OpenMP / MKL thread, fixed before torch loads: the reference's fits (linear_gaussian's
+# lstsq, the NN epochs) then reproduce bit for bit from run to run (under the default thread
+# pool the ridge weights drifted by up to 2.4e-7 between regenerations)
+os.environ["OMP_NUM_THREADS"] = "1"
+os.environ["MKL_NUM_THREADS"] = "1"
+
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -39,6 +45,7 @@ CONFIGS = ("cfg2", "cfg3", "cfg4", "cfg5", "anchor64")
 
 def fit_reference(cfg_name: str):
     from vbn import VBN, defaults
+    G.deterministic_fits()
     cfg = synthetic.CONFIGS[cfg_name]
     g = synthetic.random_dag(cfg["n_nodes"], seed=0)
     data = synthetic.sem_data(g, cfg.get("rows", 2048), seed=0)

@@ -20,6 +20,12 @@ import argparse
 import os
 import sys
 
+# one OpenMP / MKL thread, fixed before torch loads: the reference's fits (linear_gaussian's
+# lstsq, the NN epochs) then reproduce bit for bit from run to run (under the default thread
+# pool the ridge weights drifted by up to 2.4e-7 between regenerations)
+os.environ["OMP_NUM_THREADS"] = "1"
+os.environ["MKL_NUM_THREADS"] = "1"
+
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -40,6 +46,7 @@ def main():
     os.environ.setdefault("CI", "1")
     import networkx as nx
     import vbn as vbn_mod
+    G.deterministic_fits()
 
     g = nx.DiGraph()
     g.add_edges_from([("a", "b"), ("a", "c"), ("b", "c"), ("c", "d"), ("c", "e"), ("d", "e"), ("e", "f"),
