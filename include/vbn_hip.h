@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 11
+#define VBN_ABI_VERSION 12
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001

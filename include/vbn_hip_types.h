@@ -73,6 +73,10 @@ enum vbn_role {
                                    precomp_q [B][stride] (row b; aux2 as above); needs
                                    n_samples a multiple of 64 (one query per wave)            */
 
+#define VBN_F_CLAMP_EV 65536    /* (ABI v12) fixed role: the value read from the fixed buffer is
+                                   clamped as likelihood weighting's clamp_evidence does
+                                   (_core.py:112-114): NaN -> 0, then [-1e6, 1e6]            */
+
 /* activations of the NN CPDs (reference gaussian_nn.py:19-24) */
 enum vbn_act { VBN_ACT_RELU = 0, VBN_ACT_TANH = 1, VBN_ACT_GELU = 2, VBN_ACT_ELU = 3 };
 
@@ -95,7 +99,9 @@ enum vbn_mode {
  * split-f16 W2 | W3 | b3], rounded up to a multiple of 256 floats (params float offset,
  * length in floats), which the walk stages into LDS one step ahead (0 = the step runs no
  * MLP); the exact-f32 W2 copy (off_w2) deliberately stays outside the block and is read from
- * global memory on the rare exact path; [7] unused (-1).  KDE packs [1] (parent features) and
+ * global memory on the rare exact path; [7] = (ABI v12) kde steps: the one-feature moment
+ * table of pass 1 (plan.py kde_moment_table: header [u_lo, 1/delta, delta, n_cells] then
+ * [n_cells][16 chunks][4 terms] f32), -1 = none; -1 on every other step.  KDE packs [1] (parent features) and
  * [2] (parent ++ target features) hold the bf16x3 slots of v_mfma_f32_16x16x32_bf16
  * ([block][quarter][16 points][8 bf16], plan.py _kde_pack_bf16); [3] = per-point f32 records,
  * [4] = the packed-VALU layout. */

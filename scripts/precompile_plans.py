@@ -42,8 +42,9 @@ def plans_for(name):
     common = dict(latent=latent, fixed=fixed, out_nodes=[target], skip=[], exact_f32=False, kde_valu=False)
     if eng in ("likelihood_weighting", "importance_sampling"):
         lw = eng == "likelihood_weighting"
-        key = ("weighted", target, tuple(sorted(ev)), (), lw, False, False, False)
-        plan = E._plan(pk, key, logp=logp_ev, shared_roots=lw, mode=P.MODE_WEIGHTED, **common)
+        key = ("weighted", target, tuple(sorted(ev)), (), lw, lw, False, False, False)
+        plan = E._plan(pk, key, logp=logp_ev, shared_roots=lw, mode=P.MODE_WEIGHTED,
+                       clamp=list(ev) if lw else (), **common)
     elif eng == "ancestral":
         key = ("ancestral", target, tuple(sorted(vals)), False, False, False)
         plan = E._plan(pk, key, logp=[], shared_roots=True, mode=P.MODE_SAMPLE, **common)

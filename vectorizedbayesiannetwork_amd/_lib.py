@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (

@@ -89,6 +89,106 @@ __global__ void __launch_bounds__(NW_THREADS) vbn_normalize_kernel(const float* 
   }
 }
 
+// The same normalisation with the row held in registers (round 6): S <= NW_THREADS * PER, each
+// thread keeps PER consecutive log-weights from ONE pass of 16-byte loads, and the max, the
+// exp-sum and the normalised write + ESS all work on those registers -- one read of the row
+// instead of three.  Reductions: per-thread partials over its PER values, then wave shuffles,
+// then the 4 waves in LDS (the same tree as vbn_normalize_kernel; only each thread's share of
+// the row is contiguous instead of strided).  cfg3: 14.0 us -> (r06b) per 4096 x 1024 call.
+template <int PER>
+__global__ void __launch_bounds__(NW_THREADS) vbn_normalize_reg_kernel(const float* __restrict__ log_w,
+                                                                      float* __restrict__ w, float* __restrict__ ess,
+                                                                      int S, int normalize, float eps,
+                                                                      const int32_t* run_if, int32_t* flag,
+                                                                      float ess_thr) {
+  if (run_if && *run_if == 0) return;
+  __shared__ float red[NW_THREADS / WAVE];
+  __shared__ int nan_flag;
+  const int64_t row = blockIdx.x;
+  const float* x = log_w + row * S;
+  float* y = w + row * S;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  const int j0 = tid * PER;
+  if (tid == 0) nan_flag = 0;
+  float v[PER];
+  const bool full = j0 + PER <= S && (S & 3) == 0;
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < PER; k += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(x + j0 + k);
+      v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = j0 + k < S ? x[j0 + k] : -INFINITY;
+  }
+  float m = -INFINITY;
+  int has_nan = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    has_nan |= (v[k] != v[k]);
+    m = fmaxf(m, v[k]);
+  }
+  __syncthreads();                                   // nan_flag = 0 before any OR
+  if (has_nan) atomicOr(&nan_flag, 1);
+  m = wave_max(m);
+  if (lane == 0) red[wid] = m;
+  __syncthreads();
+  m = red[0];
+  for (int k = 1; k < NW_THREADS / WAVE; ++k) m = fmaxf(m, red[k]);
+  const bool row_nan = nan_flag != 0;
+  __syncthreads();
+  if (!normalize) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (j0 + k < S) {
+        const float e = expf(v[k] - m);               // all -inf row: exp(NaN) stays NaN
+        y[j0 + k] = row_nan ? NAN : (e != e ? e : fmaxf(e, eps));
+      }
+    }
+    return;
+  }
+  float e[PER];
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    e[k] = j0 + k < S ? expf(v[k] - m) : 0.f;
+    sum += e[k];
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[wid] = sum;
+  __syncthreads();
+  sum = 0.f;
+  for (int k = 0; k < NW_THREADS / WAVE; ++k) sum += red[k];
+  __syncthreads();
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const float q = row_nan ? NAN : e[k] / sum;      // all -inf row: (-inf)-(-inf) -> NaN
+    e[k] = q;
+    if (j0 + k < S) sq += q * q;
+  }
+  if (full) {
+#pragma unroll
+    for (int k = 0; k < PER; k += 4)
+      *reinterpret_cast<float4*>(y + j0 + k) = make_float4(e[k], e[k + 1], e[k + 2], e[k + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (j0 + k < S) y[j0 + k] = e[k];
+  }
+  sq = wave_sum(sq);
+  if (lane == 0) red[wid] = sq;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+    for (int k = 0; k < NW_THREADS / WAVE; ++k) t += red[k];
+    const float es = 1.0f / t;
+    if (ess) ess[row] = es;
+    if (flag && es < ess_thr) atomicOr(flag, 1);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // multinomial resampling (resampled_importance_sampling.py:33-41): one 256-thread workgroup per
 // query; inclusive CDF of the weights in LDS, one binary search per draw, state rows gathered
@@ -691,8 +791,23 @@ extern "C" int vbn_hip_normalize_weights_ex(const float* log_w, float* w, float*
                                             int32_t* flag, float ess_thr, void* stream) {
   if (!log_w || !w || n_queries <= 0 || n_samples <= 0 || (flag && !normalize))
     return fail(VBN_E_ARGS, "vbn_hip_normalize_weights: bad arguments");
-  hipLaunchKernelGGL(vbn_normalize_kernel, dim3((unsigned)n_queries), dim3(NW_THREADS), 0,
-                     (hipStream_t)stream, log_w, w, ess, n_samples, normalize, eps, run_if, flag, ess_thr);
+  // rows of up to 4096 weights stay in registers (vbn_normalize_reg_kernel; 16-byte loads need
+  // 16-byte aligned rows); longer rows stream three times through the strided form
+  const bool al = ((uintptr_t)log_w & 15) == 0 && ((uintptr_t)w & 15) == 0;
+  const dim3 g((unsigned)n_queries), blk(NW_THREADS);
+  hipStream_t st = (hipStream_t)stream;
+  if (al && n_samples <= NW_THREADS * 4)
+    hipLaunchKernelGGL(vbn_normalize_reg_kernel<4>, g, blk, 0, st, log_w, w, ess, n_samples, normalize, eps, run_if,
+                       flag, ess_thr);
+  else if (al && n_samples <= NW_THREADS * 8)
+    hipLaunchKernelGGL(vbn_normalize_reg_kernel<8>, g, blk, 0, st, log_w, w, ess, n_samples, normalize, eps, run_if,
+                       flag, ess_thr);
+  else if (al && n_samples <= NW_THREADS * 16)
+    hipLaunchKernelGGL(vbn_normalize_reg_kernel<16>, g, blk, 0, st, log_w, w, ess, n_samples, normalize, eps, run_if,
+                       flag, ess_thr);
+  else
+    hipLaunchKernelGGL(vbn_normalize_kernel, g, blk, 0, st, log_w, w, ess, n_samples, normalize, eps, run_if, flag,
+                       ess_thr);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;

@@ -227,6 +227,14 @@ __device__ __forceinline__ float fixed_value(const vbn_walk_args& A, const vbn_s
   return A.fixed[row * A.fixed_ld + st.fixed_col + d];
 }
 
+// likelihood weighting's clamp_evidence (_core.py:112-114) on the value read, for steps with
+// VBN_F_CLAMP_EV: the unclamped fixed buffer of importance sampling serves its fallback as is
+__device__ __forceinline__ float fixed_read(const vbn_walk_args& A, const vbn_step& st, int d, const Lane& L) {
+  const float v = fixed_value(A, st, d, L);
+  if (st.flags & VBN_F_CLAMP_EV) return v != v ? 0.f : fminf(fmaxf(v, -1e6f), 1e6f);
+  return v;
+}
+
 // VBN_F_PRECOMP: this sample's row of the node's pre-pass quantities (state_flags 4: state =
 // the one-query pre-pass walk's out_x [S][stride]; aux2 = first column | stride << 16)
 __device__ __forceinline__ const float* precomp_row(const vbn_walk_args& A, const vbn_step& st, const Lane& L) {
@@ -247,7 +255,7 @@ __device__ __forceinline__ const cfloat* precomp_qrow(const vbn_walk_args& A, co
 // value of a fixed node: from the fixed buffer, or (VBN_F_KEEP, Gibbs) the slot's current value
 __device__ __forceinline__ float node_fixed(const vbn_walk_args& A, const vbn_step& st, int d,
                                             const Lane& L) {
-  return (!L.lean && (st.flags & VBN_F_KEEP)) ? vread(L, st.out_col + d) : fixed_value(A, st, d, L);
+  return (!L.lean && (st.flags & VBN_F_KEEP)) ? vread(L, st.out_col + d) : fixed_read(A, st, d, L);
 }
 
 // ------------------------------------------------------------------------------------------

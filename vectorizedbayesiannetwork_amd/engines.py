@@ -345,8 +345,8 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
     """One launch of the particle walk; returns (lp [b,n] or empty, x [b,n,n_out_cols]).
     ``state``/``state_flags``/``step_begin``/``step_end``: one segment of a split walk;
     ``plan_jit``: ops.walk (0 interpreter, 1 plan-specialised for large lean launches, 2 always);
-    ``run_if``: device int32 [1] predicating every launch (pre-passes included; nothing runs and
-    nothing is written when it holds 0); ``out_x``: samples written into this [b, n, n_out_cols]
+    ``run_if``: device int32 [1] predicating the launch (the plain plan, no pre-passes: their
+    outputs are bit-identical; nothing runs and nothing is written when it holds 0); ``out_x``: samples written into this [b, n, n_out_cols]
     tensor (a predicated launch that does not run leaves it as it was)."""
     n_out_cols = int(plan.out_cols.numel()) if plan.out_nodes else 0
     noise_b = 1
@@ -362,8 +362,10 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
     precomp = precomp_q = None
     walk_plan = plan
     pre_ran = False
+    # a predicated launch (run_if: importance sampling's fallback, which rarely runs) walks the
+    # plain plan: its pre-passes would be two more launches of no-op waves on every call
     use_pc = (PRECOMPUTE and plan.pc is not None and noise is None and state is None and step_begin == 0
-              and step_end < 0 and n % 64 == 0 and not fixed_per_particle)
+              and step_end < 0 and n % 64 == 0 and not fixed_per_particle and run_if is None)
     pcs = _pc_state()
     if pcs["on"]:
         # VBN.precompile / pack_query: compile (or load) the specialised walk this launch would
@@ -536,30 +538,31 @@ class LikelihoodWeighting(_EngineBase):
 
     def _walk(self, vbn, query, n, *, clamp, shared_roots, kwargs, offset=0, noise=None, run_if=None, out_x=None,
               fixed_from=None):
-        """``fixed_from``: (fixed nodes, [B, fixed_ld] buffer) of an unclamped walk of the same
-        query (importance sampling's): with ``clamp`` and no do-values, this walk's buffer is
-        that one clamped as a whole (clamp_evidence, _core.py:112-114) -- two kernels instead of
-        two per evidence node plus the concatenation."""
+        """``clamp``: the evidence is clamped as clamp_evidence does (_core.py:112-114) -- by the
+        kernel as it reads the fixed buffer (VBN_F_CLAMP_EV), so no clamp kernels run; the host
+        clamps too only where the discrete-class check needs the clamped values.
+        ``fixed_from``: (fixed nodes, [B, fixed_ld] buffer) of an unclamped walk of the same query
+        (importance sampling's): with no do-values this walk reads that buffer as it is."""
         target, ev, do = self._query(query)
         b = infer_batch_size(ev, do)
         dev = _device_of(vbn)
         pk = packed_model(vbn, dev)
         model = pk.model
-        reuse = fixed_from is not None and clamp and not do and not _has_discrete(pk, list(ev))
-        vals = _fixed_values(query, dev, clamp=clamp and not reuse)
+        host_clamp = clamp and _has_discrete(pk, list(ev))
+        reuse = fixed_from is not None and not do and not host_clamp
+        vals = _fixed_values(query, dev, clamp=host_clamp)
         _check_discrete(pk, vals, list(ev))
         keep = barren_pruned(model, [target] + list(ev)) if self.prune_barren else set(model.topo)
-        key = ("weighted", target, tuple(sorted(ev)), tuple(sorted(do)), shared_roots, self.prune_barren)
+        key = ("weighted", target, tuple(sorted(ev)), tuple(sorted(do)), shared_roots, bool(clamp), self.prune_barren)
         plan = self._plan(pk, key, latent=[x for x in model.topo if x in keep and x not in vals],
                      fixed=[x for x in model.topo if x in keep and x in vals],
                      logp=[x for x in model.topo if x in ev and x in keep], out_nodes=[target],
                      shared_roots=shared_roots, mode=MODE_WEIGHTED,
-                     skip=[x for x in model.topo if x not in keep])
+                     skip=[x for x in model.topo if x not in keep],
+                     clamp=[x for x in ev if x in keep] if clamp else ())
         if reuse and tuple(fixed_from[0]) == tuple(plan.fixed_nodes):
-            fx = torch.nan_to_num(fixed_from[1], nan=0.0, posinf=1e6, neginf=-1e6).clamp_(min=-1e6, max=1e6)
+            fx = fixed_from[1]
         else:
-            if reuse:                                  # other layout: clamp per node after all
-                vals = _fixed_values(query, dev, clamp=clamp)
             fx = _fixed_buffer(plan, vals, b, dev)
         self._last_fixed = (tuple(plan.fixed_nodes), fx)
         seed = kwargs.get("_seed_value")
@@ -580,9 +583,9 @@ class LikelihoodWeighting(_EngineBase):
 
     def infer_into(self, vbn, query, n: int, *, seed: int, offset: int, run_if: torch.Tensor,
                    w_out: torch.Tensor, x_out: torch.Tensor, noise=None, fixed_from=None) -> None:
-        """The whole LW call predicated on the device flag ``run_if``: pre-passes, walk and
-        normalisation write their weights / samples into ``w_out`` / ``x_out`` when it holds 1
-        and launch as no-ops otherwise (importance sampling's fallback without a host sync)."""
+        """The whole LW call predicated on the device flag ``run_if``: walk and normalisation
+        write their weights / samples into ``w_out`` / ``x_out`` when it holds 1 and launch as
+        no-ops otherwise (importance sampling's fallback without a host sync)."""
         log_w, _ = self._walk(vbn, query, n, clamp=True, shared_roots=True, kwargs={"_seed_value": seed},
                               offset=offset, noise=noise, run_if=run_if, out_x=x_out, fixed_from=fixed_from)
         ops.normalize_weights_ex(log_w, self.normalize, self.eps, run_if=run_if, w_out=w_out)

@@ -14,6 +14,7 @@ buffer the kernel indexes is large enough before the launch.
 from __future__ import annotations
 
 import ctypes
+import threading
 from typing import Optional, Tuple
 
 import torch
@@ -395,6 +396,30 @@ def normalize_weights(log_w: Tensor, normalize: bool, eps: float) -> Tuple[Tenso
     return w, ess
 
 
+# The ESS fallback flags: a zeroed device pool per GPU handed out one int32 slot per call, and
+# zeroed again (one fill) after FLAG_SLOTS calls -- instead of one zero-fill launch per call
+# (~5 us of GPU time each on a busy queue, r06a cfg3 trace).  Stream order keeps a slot's
+# readers (the predicated fallback launches) ahead of the refill; a returned flag stays valid
+# for the next FLAG_SLOTS - 1 calls on its device.
+FLAG_SLOTS = 4096
+_FLAG_POOLS: dict = {}
+_FLAG_LOCK = threading.Lock()
+
+
+def _flag_slot(device: torch.device) -> Tensor:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    with _FLAG_LOCK:
+        ent = _FLAG_POOLS.get(idx)
+        if ent is None:
+            ent = _FLAG_POOLS[idx] = [torch.zeros(FLAG_SLOTS, device=device, dtype=torch.int32), 0]
+        elif ent[1] >= FLAG_SLOTS:
+            ent[0].zero_()
+            ent[1] = 0
+        k = ent[1]
+        ent[1] += 1
+        return ent[0][k:k + 1]
+
+
 def normalize_weights_ex(log_w: Tensor, normalize: bool, eps: float, *, ess_thr: Optional[float] = None,
                          run_if: Optional[Tensor] = None, w_out: Optional[Tensor] = None,
                          ess_out: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
@@ -420,7 +445,7 @@ def normalize_weights_ex(log_w: Tensor, normalize: bool, eps: float, *, ess_thr:
     if ess_thr is not None:
         if not normalize:
             raise ValueError("vbn_hip::normalize_weights: the ESS flag needs normalize=True")
-        flag = torch.zeros(1, device=log_w.device, dtype=torch.int32)
+        flag = _flag_slot(log_w.device)
     lib = _lib.load()
     with torch.cuda.device(log_w.device):
         _lib.check(lib.vbn_hip_normalize_weights_ex(
@@ -732,7 +757,8 @@ def is_lw(plan: Tensor, params: Tensor, fixed: Tensor, n_samples: int, seed: int
           q_base: int = 0, noise: Optional[Tensor] = None, lw_mode: bool = False, normalize: bool = True,
           eps: float = 0.0, ess_threshold: float = 0.1, plan_jit: int = 1) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """Importance sampling (lw_mode False: the plan's roots drawn per query, evidence raw) or
-    likelihood weighting (True: shared roots, the caller clamps the evidence) of a packed
+    likelihood weighting (True: shared roots; the packed LW plan clamps the evidence as it reads
+    it, VBN_F_CLAMP_EV, so a caller's own clamp is harmless but not needed) of a packed
     weighted plan -> (weights [B,S], samples [B,S,Dt], ess [B], fallback flag (device bool): IS
     -- some ESS below max(1, ess_threshold S), NaN never triggers; LW -- False).  As the
     reference, the fallback re-draw with LW is the caller's (its plan is another signature)."""

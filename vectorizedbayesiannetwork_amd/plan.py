@@ -52,6 +52,7 @@ F_HEAD_MFMA = 4096
 F_PRECOMP = 8192          # csrc VBN_F_PRECOMP: per-sample quantities read from the pre-pass
 F_PRE_OUT = 16384         # csrc VBN_F_PRE_OUT: the pre-pass writes a node's per-sample quantities
 F_PRECOMP_Q = 32768       # csrc VBN_F_PRECOMP_Q: with F_PRECOMP, per-QUERY quantities (precomp_q)
+F_CLAMP_EV = 65536        # csrc VBN_F_CLAMP_EV: fixed value clamped in the kernel (clamp_evidence)
 MAX_NODES = 1 << 14
 MAX_NODE_DIMS = 1 << 8
 
@@ -640,7 +641,7 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
                logp: Sequence[str], out_nodes: Sequence[str], shared_roots: bool, mode: int,
                skip: Sequence[str] = (), exact_f32: bool = False, kde_valu: bool = False,
                params: Sequence[str] = (), pre_out: Sequence[str] = (),
-               order: Optional[Sequence[str]] = None) -> QueryPlan:
+               order: Optional[Sequence[str]] = None, clamp: Sequence[str] = ()) -> QueryPlan:
     """Step table for one query signature.
 
     ``latent``: nodes sampled; ``fixed``: nodes read from the fixed buffer (evidence/do);
@@ -657,12 +658,14 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
     chunk sums ++ the underflow shift.  ``order``: the walk order of the non-skipped nodes (a
     topological order; default the model's, reference ``vbn.py:670-675``) -- every draw is keyed
     by its node, so the order changes only the LDS slot assignment and the Box-Muller pairing
-    (:func:`liveness_order`).
+    (:func:`liveness_order`).  ``clamp``: fixed nodes whose values the kernel clamps as
+    likelihood weighting's clamp_evidence does (VBN_F_CLAMP_EV; _core.py:112-114).
     """
     model = packed.model
     latent_s, fixed_s, logp_s, skip_s = set(latent), set(fixed), set(logp), set(skip)
     params_s = set(params)
     pre_s = set(pre_out)
+    clamp_s = set(clamp)
     if order is None:
         order = [n for n in model.topo if n not in skip_s]
     else:
@@ -762,6 +765,8 @@ def build_plan(packed: PackedModel, *, latent: Sequence[str], fixed: Sequence[st
             fl |= F_KDE_VALU
         if n in pre_s:
             fl |= F_PRE_OUT
+        if n in clamp_s and n in fixed_s:
+            fl |= F_CLAMP_EV
         row[S_FLAGS] = fl
         row[S_ACT] = npk.act
         row[S_NIN] = npk.n_in
@@ -1282,6 +1287,7 @@ def precompute_plans(packed: PackedModel, plan: QueryPlan, *, skip: Sequence[str
         for i, n in enumerate(qorder):
             if n not in cq:
                 qrow[i][S_FIXEDCOL] = rows[at[n]][S_FIXEDCOL]
+                qrow[i][S_FLAGS] |= rows[at[n]][S_FLAGS] & F_CLAMP_EV    # LW: clamped evidence
         import dataclasses
         pre_q = dataclasses.replace(_with_steps(pre_q, qrow, packed.device), fixed_nodes=list(plan.fixed_nodes),
                                     fixed_ld=plan.fixed_ld)
