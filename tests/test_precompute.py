@@ -28,13 +28,14 @@ def _plan(cfg_name, engine="mcm"):
 
 def _want(model, vals, plan, shared):
     """nodes the precompute must mark: per sample (parents all shared latent roots) and per
-    query (parents all evidence); NN kinds latent or evidence with a log-prob, KDE latent"""
+    query (parents all evidence); NN kinds latent or evidence with a log-prob, KDE latent
+    without a moment table (a table makes the chunk sums cheap in the walk itself)"""
     rows = plan.steps._vbn_host[0]
     roots = {n for n in model.topo if not model.parents[n] and n not in vals} if shared else set()
     ws, wq = set(), set()
     for i, n in enumerate(model.topo):
         kind = model.cpds[n].kind
-        if not model.parents[n] or kind not in NN_KDE:
+        if not model.parents[n] or kind not in NN_KDE or (kind == "kde" and rows[i][P.S_RES7] >= 0):
             continue
         latent = n not in vals
         if not latent and not (kind != "kde" and rows[i][P.S_FLAGS] & P.F_LOGP):

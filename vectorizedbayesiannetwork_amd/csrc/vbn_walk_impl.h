@@ -1538,36 +1538,6 @@ __device__ __forceinline__ double kde_pass1(const bf16x8* __restrict__ pa, int c
   return tot;
 }
 
-// Pass 1 of a one-feature node from its moment table (plan.kde_moment_table, round 6): around
-// the grid centre u_g nearest u = 2 x', S_c(u) = sum_k d^k T[g][c][k] with d = u - u_g, where
-// T[g][c][k] = sum_{j in c} exp2(u_g y'_j - |y'_j|^2) (ln2 y'_j)^k / k! (float64 sums, host).
-// The series' remainder is < 3e-8 of every weight (KDE_MT_Z), so the chunk sums equal the
-// exp-by-exp sums to f32 rounding -- and cost KDE_MT_TERMS - 1 FMAs and one 16-byte load per
-// chunk instead of one v_exp_f32 and half a v_pk_add_f32 per point.  The factored form (shift
-// 0): the caller takes this path only when every lane has fform.  Returns false (the wave then
-// runs the MFMA pass) when some lane's u lies outside the grid (or is NaN).
-// Table: header [u_lo, 1 / delta, delta, n_cells (int32 bits)], rows [n_cells][KDE_CHUNKS][4].
-__device__ __forceinline__ bool kde_pass1_moments(const float* __restrict__ T, float u, const Lane& L,
-                                                  double& tot) {
-  const cfloat* H = CP(T);
-  const float u_lo = H[0], inv_d = H[1], dlt = H[2];
-  const float n_cells = (float)__float_as_int(H[3]);
-  const float gr = rintf((u - u_lo) * inv_d);           // nearest centre (NaN u: not in range)
-  const bool in = gr >= 0.f && gr < n_cells;
-  if (!__all(in)) return false;
-  const float d = u - fmaf(gr, dlt, u_lo);              // the centre exactly as the host formed it
-  const float4* __restrict__ row = reinterpret_cast<const float4*>(T + 4) + (int)gr * KDE_CHUNKS;
-  tot = 0.0;
-#pragma unroll
-  for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
-    const float4 c = row[ch];
-    const float cs = fmaf(fmaf(fmaf(c.w, d, c.z), d, c.y), d, c.x);
-    L.scr[ch * WAVE + L.lane] = cs;
-    tot += (double)cs;
-  }
-  return true;
-}
-
 // Sum over all nb32 blocks of a log-density pack (kde_logp_mfma)
 template <int KG, int PG>
 __device__ __forceinline__ float kde_sum_all(const bf16x8* __restrict__ pa, int nb32, const Lane& L,
@@ -1648,6 +1618,63 @@ __device__ __forceinline__ int kde_scan(const float4* __restrict__ rec, const fl
   return min(max(back ? j1 - 1 - kh : j0 + kh, 0), M - 1);
 }
 
+// One-feature node with a moment table (plan.kde_moment_table, round 6): the index of
+// kde.py:172-178 without pass 1's exps.  Around the grid centre u_g nearest u = 2 x', a chunk's
+// sum is S_c(u) = sum_k d^k T[g][c][k] with d = u - u_g and
+// T[g][c][k] = sum_{j in c} exp2(u_g y'_j - |y'_j|^2) (ln2 y'_j)^k / k! (float64 sums, host);
+// the series' remainder is < 3e-8 of every weight (plan.KDE_MT_Z), so the sums equal the
+// exp-by-exp ones to f32 rounding, at one 16-byte load and 3 FMAs per chunk.  Per cell the
+// table holds the chunks (~M/64 points each), their groups of 8 and the whole point set: the
+// threshold u * total, then the group whose running sum passes it, then the chunk inside it
+// (<= 8 + 8 sums instead of 64), so the scan that follows covers about M/128 points instead of
+// the MFMA pass's M/32; a crossing past the last group or chunk (rounding) takes the last.
+// Factored form (shift 0): the caller takes this path only when every lane has fform.  Returns
+// -1 for the whole wave when some lane's u is off the grid (or NaN): the MFMA pass then runs.
+// Table: header [u_lo, 1 / delta, delta, n_cells, n_chunks, chunk points (int32 bits), 0, 0],
+// rows [n_cells][n_chunks + n_groups + 1] float4 (plan.kde_moment_table).
+#define KDE_MT_HEAD 8         // header floats (plan.KDE_MT_HEADER)
+#define KDE_MT_GROUP 8        // chunks per group (plan.KDE_MT_GROUP)
+__device__ __forceinline__ int kde_index_moments(const float* __restrict__ T, float xb0, float ucat,
+                                                 const float4* __restrict__ rec, int M) {
+  const cfloat* H = CP(T);
+  const float u_lo = H[0], inv_d = H[1], dlt = H[2];
+  const int n_cells = __float_as_int(H[3]), nch = __float_as_int(H[4]), per = __float_as_int(H[5]);
+  const float gr = rintf((xb0 - u_lo) * inv_d);          // nearest centre (NaN u: not in range)
+  const bool in = gr >= 0.f && gr < (float)n_cells;
+  if (!__all(in)) return -1;
+  const float d = xb0 - fmaf(gr, dlt, u_lo);             // the centre exactly as the host formed it
+  const int ng = (nch + KDE_MT_GROUP - 1) / KDE_MT_GROUP;
+  const float4* __restrict__ row = reinterpret_cast<const float4*>(T + KDE_MT_HEAD) + (int)gr * (nch + ng + 1);
+  auto poly = [&](const float4 c) { return fmaf(fmaf(fmaf(c.w, d, c.z), d, c.y), d, c.x); };
+  const double thr = (double)ucat * (double)poly(row[nch + ng]);
+  double cum = 0.0;
+  float gs = 0.f;
+  int g = ng - 1;
+  bool hit = false;
+  for (int k = 0; k < ng; ++k) {                        // the group
+    gs = poly(row[nch + k]);
+    const double nx = cum + (double)gs;
+    if (nx > thr) { g = k; hit = true; break; }
+    cum = nx;
+  }
+  if (!hit) cum -= (double)gs;                             // the last group
+  const int c1 = min(nch, (g + 1) * KDE_MT_GROUP);
+  int ch = c1 - 1;
+  float cs = 0.f;
+  hit = false;
+  for (int c = g * KDE_MT_GROUP; c < c1; ++c) {          // the chunk inside it
+    cs = poly(row[c]);
+    const double nx = cum + (double)cs;
+    if (nx > thr) { ch = c; hit = true; break; }
+    cum = nx;
+  }
+  if (!hit) cum -= (double)cs;                             // the group's last chunk
+  const int j0 = min(M, ch * per), j1 = min(M, j0 + per);
+  const float4* __restrict__ rev = rec + (((M + 15) >> 4) * 16 + KDE_REC_TAIL);
+  return kde_scan(rec, rev, M, j0, j1, (float)(thr - cum), cs,
+                  [&](const float4 r) { return fmaf(r.y, -1.f, fmaf(r.x, xb0, -0.f)); });
+}
+
 // Latent non-root KDE node, parent dims 1..3: index ~ softmax_j log K_p (kde.py:172-178).
 // Pass 1 (MFMA): per-chunk weight sums -> scr[chunk][lane]; pass 2 (VALU replica): locate the
 // chunk holding u * total, scan it.  All-underflow particles (every weight 0) redo the sums on
@@ -1663,6 +1690,16 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   float xv[4] = {0.f, 0.f, 0.f, 0.f};
   const float negsq = kde_own(L, slots, scl, nf, xv);
   const bool pre = (st.flags & VBN_F_PRECOMP) != 0;
+  // per-point records (4 weight-0 rows before the first point), then the reversed copy
+  const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
+  if (nf == 1 && KDE_MT(st) >= 0 && !(st.flags & (VBN_F_PRECOMP | VBN_F_PRE_OUT)) &&
+      __all(-negsq <= KDE_FFORM_MAX)) {               // a one-feature node with a moment table
+    const int idx = kde_index_moments(L.P + KDE_MT(st), 2.f * xv[0], ucat, rec, M);
+    if (idx >= 0) {                                   // the whole wave took it
+      wave_sync();
+      return idx;
+    }
+  }
   float shift = 0.f;                                  // sigma: the sums are of exp2(a' - sigma)
   if (pre) {                                          // pass 1 of this sample / query, pre-pass
     if (st.flags & VBN_F_PRECOMP_Q) {
@@ -1692,10 +1729,7 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
     const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
     const bool fform = __all(-negsq <= KDE_FFORM_MAX);
     shift = fform ? 0.f : -negsq;
-    // one-feature nodes with a moment table: pass 1 from the table (kde_pass1_moments)
-    const bool mom = nf == 1 && fform && KDE_MT(st) >= 0 && kde_pass1_moments(L.P + KDE_MT(st), 2.f * xv[0], L, tot);
-    if (mom) {
-    } else if (nf == 1)
+    if (nf == 1)
       tot = kde_pass1<1, 1>(pa, cb >> 1, L, slots, scl, nf, fform);
     else if (nf == 2 && fform)
       tot = kde_pass1<1, 2>(pa, cb >> 1, L, slots, scl, nf, fform);
@@ -1704,8 +1738,6 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   }
   const int nfr = nf;                                 // replica form of the pass-1 elements
   const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
-  // per-point records (4 weight-0 rows before the first point), then the reversed copy
-  const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
   if (!pre && !(tot > 0.0)) {                         // every weight underflowed (or NaN parent)
     float amax = -INFINITY;
     for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_rec(rec[j], xb0, xb1, xb2, 0.f, nfr));

@@ -192,20 +192,25 @@ def _kde_pack_valu(y: np.ndarray) -> np.ndarray:
     return a.reshape(-1, 8, nf).transpose(0, 2, 1)
 
 
-# ---- moment tables of one-feature KDE nodes (csrc kde_pass1_moments, round 6) ---------------
-# Pass 1 needs, per particle u = 2 x' and chunk c, S_c(u) = sum_{j in c} exp2(u y'_j - |y'_j|^2).
-# Around a grid centre u_g, exp2(u y') = exp2(u_g y') * exp(d ln2 y') with d = u - u_g, so
+# ---- moment tables of one-feature KDE nodes (csrc kde_index_moments, round 6) ---------------
+# Sampling needs, per particle u = 2 x' and chunk c, S_c(u) = sum_{j in c} exp2(u y'_j - |y'_j|^2)
+# (the factored form of kde.py:172-177's softmax weights).  Around a grid centre u_g,
+# exp2(u y') = exp2(u_g y') * exp(d ln2 y') with d = u - u_g, so
 #   S_c(u) = sum_k d^k T[g][c][k],   T[g][c][k] = sum_{j in c} exp2(u_g y'_j - |y'_j|^2) (ln2 y'_j)^k / k!
 # truncated after KDE_MT_TERMS terms: the remainder of each point's series is below
-# |z|^K / K! e^|z| with |z| = |d| ln2 |y'_j| <= KDE_MT_Z, i.e. a relative error < KDE_MT_EPS on
-# every weight, all of the same sign -- below the f32 rounding of a 640-term chunk sum.
+# |z|^K / K! e^|z| with |z| = |d| ln2 |y'_j| <= KDE_MT_Z, i.e. a relative error < 3e-8 on every
+# weight, all of the same sign -- below the f32 rounding of the chunk sums.  The chunks are finer
+# than the MFMA pass's 16 (KDE_MT_CHUNKS, ~M/64 points each), since a chunk costs 3 FMAs
+# instead of its points' exps and the inverse-CDF scan then covers ~M/128 points instead of ~M/32.
 KDE_MOMENTS = os.environ.get("VBN_KDE_MOMENTS", "1") != "0"      # A/B: 0 = MFMA pass 1 for every node
 KDE_MT_TERMS = 4
 KDE_MT_Z = 0.028                 # |d| ln2 max|y'| at the cell edge: 0.028^4 / 24 * e^0.028 < 3e-8
-KDE_MT_MAX_CELLS = 16384         # table size bound (16384 x 16 x 4 floats = 4 MiB per node)
+KDE_MT_CHUNKS = 64               # inverse-CDF chunks of a moment-table node (at most)
+KDE_MT_MAX_CELLS = 16384         # table size bound (cells x 65 rows x 16 B: <= 17 MiB per node)
 KDE_MT_EXP_MAX = 100.0           # largest log2 weight a cell may hold (f32 sums stay finite)
 KDE_MT_EXP_MIN = -80.0           # every cell keeps a weight above 2^-80 (no all-underflow chunk set)
-KDE_MT_HEADER = 4                # floats: u_lo, 1 / delta, delta, n_cells (int32 bits)
+KDE_MT_HEADER = 8                # floats: u_lo, 1 / delta, delta, n_cells, n_chunks, chunk points
+                                 # (the last three int32 bits), 0, 0
 
 
 def kde_moment_cells(y: np.ndarray):
@@ -244,10 +249,26 @@ def kde_moment_centres(lo32, delta32, n: int) -> np.ndarray:
     return (g * np.float64(delta32) + np.float64(lo32)).astype(np.float32).astype(np.float64)
 
 
-def kde_moment_table(y: np.ndarray, m_chunk: int) -> Optional[np.ndarray]:
-    """The moment table of one-feature KDE parent points y' (float32, scaled) with chunks of
-    ``m_chunk`` points (the inverse-CDF chunks: _kde_cb(M) * 16): header [u_lo, 1 / delta,
-    delta, n_cells (int32 bits)] then [n_cells][KDE_CHUNKS][KDE_MT_TERMS] float32 (float64
+def kde_moment_chunks(m: int) -> Tuple[int, int]:
+    """(chunks, points per chunk) of a moment-table node of m points: ceil(m / 64) points per
+    chunk, as many chunks as that takes (every chunk holds a point)."""
+    per = -(-m // KDE_MT_CHUNKS)
+    return -(-m // per), per
+
+
+KDE_MT_GROUP = 8                 # chunks per group (the kernel locates a group, then its chunk)
+
+
+def kde_moment_rows(n_chunks: int) -> int:
+    """Rows per cell: the chunks, their groups of KDE_MT_GROUP, the whole point set."""
+    return n_chunks + -(-n_chunks // KDE_MT_GROUP) + 1
+
+
+def kde_moment_table(y: np.ndarray) -> Optional[np.ndarray]:
+    """The moment table of one-feature KDE parent points y' (float32, scaled): header
+    [u_lo, 1 / delta, delta, n_cells, n_chunks, chunk points (int32 bits), 0, 0], then per cell
+    the n_chunks chunk rows, one row per group of KDE_MT_GROUP chunks and one row for the whole
+    point set, KDE_MT_TERMS float32 each ([n_cells][kde_moment_rows(n_chunks)][4]; float64
     sums, one rounding).  None when kde_moment_cells declines the node."""
     cells = kde_moment_cells(y)
     if cells is None:
@@ -256,17 +277,24 @@ def kde_moment_table(y: np.ndarray, m_chunk: int) -> Optional[np.ndarray]:
     y64 = np.asarray(y, np.float32).reshape(-1).astype(np.float64)
     sq = (y64 * y64).astype(np.float32).astype(np.float64)
     m = y64.size
+    nch, per = kde_moment_chunks(m)
     centres = kde_moment_centres(lo32, delta32, n)
     pw = np.stack([(math.log(2.0) * y64) ** k / math.factorial(k) for k in range(KDE_MT_TERMS)], axis=1)
-    tab = np.zeros((n, KDE_CHUNKS, KDE_MT_TERMS), np.float64)
-    for c in range(KDE_CHUNKS):
-        j0, j1 = min(m, c * m_chunk), min(m, (c + 1) * m_chunk)
-        if j0 >= j1:
-            continue
+    ng = -(-nch // KDE_MT_GROUP)
+    tab = np.zeros((n, kde_moment_rows(nch), KDE_MT_TERMS), np.float64)
+    for j0 in range(0, m, 4096):                               # bounded [cells x points] blocks
+        j1 = min(m, j0 + 4096)
         wts = np.exp2(centres[:, None] * y64[None, j0:j1] - sq[None, j0:j1])     # [n, pts]
-        tab[:, c, :] = wts @ pw[j0:j1]
-    head = np.array([lo32, inv32, delta32, 0], np.float32)
-    head[3:4] = np.array([n], np.int32).view(np.float32)
+        contrib = wts[:, :, None] * pw[None, j0:j1, :]                           # [n, pts, K]
+        chunk = np.arange(j0, j1) // per
+        for c in np.unique(chunk):
+            tab[:, c, :] += contrib[:, chunk == c, :].sum(axis=1)
+    for g in range(ng):
+        tab[:, nch + g, :] = tab[:, g * KDE_MT_GROUP:min(nch, (g + 1) * KDE_MT_GROUP), :].sum(axis=1)
+    tab[:, nch + ng, :] = tab[:, :nch, :].sum(axis=1)
+    head = np.zeros(KDE_MT_HEADER, np.float32)
+    head[:3] = [lo32, inv32, delta32]
+    head[3:6] = np.array([n, nch, per], np.int32).view(np.float32)
     return np.concatenate([head, tab.astype(np.float32).reshape(-1)])
 
 
@@ -471,8 +499,8 @@ def _pack_node(blob: _Blob, rec: CPDRecord) -> NodePack:
             offs["kq"] = blob.add(_kde_pack_b32(_np(pts_p) * c_p))
             offs["kr"] = blob.add(_kde_pack([_np(pts_p) * c_p], records=True))
             offs["kv"] = blob.add(_kde_pack_valu(_np(pts_p) * c_p))
-            if dp == 1 and KDE_MOMENTS:               # pass 1 from a moment table (kde_pass1_moments)
-                mt = kde_moment_table((_np(pts_p) * c_p).reshape(-1), _kde_cb(m) * 16)
+            if dp == 1 and KDE_MOMENTS:               # pass 1 from a moment table (kde_index_moments)
+                mt = kde_moment_table((_np(pts_p) * c_p).reshape(-1))
                 if mt is not None:
                     offs["kmt"] = blob.add(mt)
         if dp + D <= 4:
@@ -1249,8 +1277,10 @@ def precompute_plans(packed: PackedModel, plan: QueryPlan, *, skip: Sequence[str
         kind, role = int(r[S_KIND]), int(r[S_ROLE])
         if kind in nn_kinds and not r[S_FLAGS] & F_MLP_GENERIC:
             return role == ROLE_LATENT or (role == ROLE_FIXED and bool(r[S_FLAGS] & F_LOGP))
+        # a KDE node with a moment table computes its chunk sums from the table in a few FMAs;
+        # precomputing them would only force the pre-pass's 16 coarse chunks on its scan
         return (kind == KIND_ID["kde"] and role == ROLE_LATENT and not r[S_FLAGS] & F_KDE_VALU
-                and r[S_OFF_KQ] >= 0)
+                and r[S_OFF_KQ] >= 0 and r[S_RES7] < 0)
 
     cand_s = [n for n in order if qualifies(n) and all(p in root_s for p in model.parents[n])]
     cand_q = [n for n in order if per_query and qualifies(n) and all(p in fixed_s for p in model.parents[n])]
