@@ -24,7 +24,10 @@
  *                             KDECPD          (vbn/cpds/kde.py:105-182)
  *                             SoftmaxNNCPD    (vbn/cpds/softmax_nn.py:581-759).
  *   vbn_hip_posterior_stats VBN._posterior_stats (vbn/vbn.py:483-504), the summary behind
- *                             VBN.infer_relative (vbn/vbn.py:519-568)
+ *                             VBN.infer_relative (vbn/vbn.py:519-568); fused forms (ABI v13):
+ *                             the MCM walk's epilogue partials (vbn_walk_args.stats_part) +
+ *                             vbn_hip_posterior_stats_merge, and the IS / LW normalisation's
+ *                             vbn_hip_normalize_weights_stats
  *   vbn_hip_walk (mode GIBBS)  GibbsSampler.sample sweeps (vbn/sampling/gibbs.py:23-92):
  *                             8 candidates per chain drawn by the node's CPD, scored with the
  *                             node's and its children's log-probs, one chosen per chain
@@ -50,7 +53,7 @@
 extern "C" {
 #endif
 
-#define VBN_ABI_VERSION 12
+#define VBN_ABI_VERSION 13
 
 /* error codes besides hipError_t values */
 #define VBN_E_ARGS 1001
@@ -124,6 +127,23 @@ int vbn_hip_resample(const float* w, const float* u, uint64_t seed, uint64_t off
  *   ess[b] = 1 / max(sum_s w^2, eps).   pdf [B][S], x [B][S][D] contiguous. */
 int vbn_hip_posterior_stats(const float* pdf, const float* x, float* mean, float* std, float* ess,
                             int64_t n_queries, int32_t n_samples, int32_t dim, float eps, void* stream);
+
+/* (ABI v13) The same summary finished from a lean MCM walk's epilogue partials
+ * (vbn_walk_args.stats_part, n_parts = S / 64 rows of 2 + 4 dim doubles per query): Chan's merge
+ * of the waves' (W, m_w, M2_w) -- or of (64, m_u, M2_u) where W <= eps, the reference's uniform
+ * weights -- in float64; mean / std [B][dim], ess [B] float32 as vbn_hip_posterior_stats. */
+int vbn_hip_posterior_stats_merge(const double* part, int64_t n_queries, int32_t n_parts, int32_t dim, float eps,
+                                  float* mean, float* std, float* ess, void* stream);
+
+/* (ABI v13) vbn_hip_normalize_weights_ex with the posterior summary of the weights it writes
+ * fused into the same pass (importance_sampling.py:82-84 / likelihood_weighting.py:75-80, then
+ * vbn.py:483-504 on (w, x)): the row stays in registers, x [B][S][dim] is read once more for
+ * the centred second moment.  mean / std [B][dim], stats_ess [B]; stats_eps is
+ * _posterior_stats' eps.  Needs n_samples <= 4096 (else VBN_E_ARGS: use the two calls). */
+int vbn_hip_normalize_weights_stats(const float* log_w, float* w, float* ess, int64_t n_queries, int32_t n_samples,
+                                    int32_t normalize, float eps, const int32_t* run_if, int32_t* flag,
+                                    float ess_thr, const float* x, int32_t dim, float stats_eps, float* mean,
+                                    float* std, float* stats_ess, void* stream);
 
 /* (ABI v10) Discrete weighted histogram per query (benchmarking/models/vbn.py:202-242):
  *   for s in order: skip a non-finite w[b][s]; i = rint(x[b][s]) (half to even); skip i

@@ -166,6 +166,16 @@ typedef struct vbn_walk_args {
                               launch returns at once and nothing is written (the importance-
                               sampling -> likelihood-weighting fallback, decided on the device
                               without a host round trip)                                 */
+  double* stats_part;      /* (ABI v13) NULL, or the posterior-summary partials of a lean MCM
+                              walk (VBN._posterior_stats, vbn/vbn.py:483-504, fused into the
+                              walk's epilogue; needs n_samples % 64 == 0, n_out_cols <= 15):
+                              per query b and wave k of its S / 64 waves, the row
+                              stats_part[(b * S/64 + k) * (2 + 4 D)] of float64
+                              [W, Q, then per output column d: m_w, M2_w, m_u, M2_u] with
+                              w = pdf nan/inf -> 0 clamped >= 0, W = sum w, Q = sum w^2,
+                              m_w = sum w x / W (0 when W = 0), M2_w = sum w (x - m_w)^2,
+                              m_u = sum x / 64, M2_u = sum (x - m_u)^2 over the wave's 64
+                              particles; vbn_hip_posterior_stats_merge finishes them      */
 } vbn_walk_args;
 
 #endif /* VBN_HIP_TYPES_H */

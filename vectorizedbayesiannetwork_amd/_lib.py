@@ -12,7 +12,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VBN_HIP_LIB", os.path.join(HERE, "libvbn_hip.so"))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 # exported symbols declared in include/vbn_hip.h
 EXPORTS = (
@@ -24,6 +24,8 @@ EXPORTS = (
     "vbn_hip_rb_epilogue",
     "vbn_hip_resample",
     "vbn_hip_posterior_stats",
+    "vbn_hip_posterior_stats_merge",
+    "vbn_hip_normalize_weights_stats",
     "vbn_hip_discrete_posterior",
     "vbn_hip_discrete_posterior_typed",
     "vbn_hip_lds_bytes",
@@ -73,6 +75,7 @@ class VbnWalkArgs(ctypes.Structure):
         ("wave_particles", ctypes.c_int32),
         ("precomp_q", ctypes.c_void_p),
         ("run_if", ctypes.c_void_p),
+        ("stats_part", ctypes.c_void_p),
     ]
 
 
@@ -127,6 +130,16 @@ def load(path: str = None) -> ctypes.CDLL:
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
         lib.vbn_hip_posterior_stats.restype = ctypes.c_int
+        lib.vbn_hip_posterior_stats_merge.argtypes = [
+            ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        lib.vbn_hip_posterior_stats_merge.restype = ctypes.c_int
+        lib.vbn_hip_normalize_weights_stats.argtypes = [
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+            ctypes.c_int32, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+            ctypes.c_void_p, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p]
+        lib.vbn_hip_normalize_weights_stats.restype = ctypes.c_int
         lib.vbn_hip_discrete_posterior.argtypes = [
             ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]

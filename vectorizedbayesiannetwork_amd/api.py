@@ -15,6 +15,8 @@ Training (``fit``/``update``) stays with the reference; this package consumes it
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 from types import SimpleNamespace
 from typing import Any, Dict, List, Optional
@@ -364,6 +366,23 @@ class VBN:
         mean, std, ess = ops.posterior_stats(pdf, samples, float(eps))
         return {"mean": mean, "std": std, "ess": ess}
 
+    def _infer_stats(self, q, eps: float, kwargs) -> Dict[str, torch.Tensor]:
+        """infer_posterior + _posterior_stats (vbn.py:536-539) with the summary fused into the
+        engine's reduction where it has one: the MCM walk's epilogue partials
+        (vbn_walk_args.stats_part + vbn_hip_posterior_stats_merge) or the IS / LW normalisation
+        (vbn_hip_normalize_weights_stats).  Other engines, sharded engines and shapes the fused
+        forms do not take (S % 64 != 0 for MCM, S > 4096 for IS / LW) run the separate pass."""
+        from .engines import ImportanceSampling, LikelihoodWeighting, MonteCarloMarginalization
+        if self._inference is None:
+            raise RuntimeError("Call set_inference_method(...) before infer_posterior().")
+        fused = (type(self._inference) in (MonteCarloMarginalization, LikelihoodWeighting, ImportanceSampling)
+                 and os.environ.get("VBN_FUSED_STATS", "1") != "0")        # 0: A/B against the separate pass
+        st = {"eps": float(eps)} if fused else None
+        pdf, samples = self.infer_posterior(q, **kwargs, **({"_stats": st} if fused else {}))
+        if st is not None and "mean" in st:
+            return {"mean": st["mean"], "std": st["std"], "ess": st["ess"]}
+        return self._posterior_stats(pdf, samples, eps=eps)
+
     @staticmethod
     def _broadcast_batch(a: torch.Tensor, b: torch.Tensor):
         """reference vbn.py:506-517"""
@@ -384,10 +403,8 @@ class VBN:
         rq = self._normalize_query(reference_query)
         if rq.target != q.target:
             raise ValueError("query and reference_query must have the same target node.")
-        qp, qs = self.infer_posterior(q, **kwargs)
-        rp, rs = self.infer_posterior(rq, **kwargs)
-        qst = self._posterior_stats(qp, qs, eps=eps)
-        rst = self._posterior_stats(rp, rs, eps=eps)
+        qst = self._infer_stats(q, eps, kwargs)
+        rst = self._infer_stats(rq, eps, kwargs)
         q_mean, r_mean = self._broadcast_batch(qst["mean"], rst["mean"])
         q_std, r_std = self._broadcast_batch(qst["std"], rst["std"])
         q_ess, r_ess = self._broadcast_batch(qst["ess"], rst["ess"])

@@ -25,6 +25,80 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// sum over the NW_THREADS threads of a workgroup (every thread gets the total)
+__device__ __forceinline__ float nw_block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int k = 0; k < NW_THREADS / WAVE; ++k) t += red[k];
+  return t;
+}
+
+// (ABI v13) the posterior summary fused into the normalisation (vbn_hip_normalize_weights_stats)
+struct vbn_stats_out {
+  const float* x;     // [B][S][dim] samples, or NULL: no summary
+  float* mean;        // [B][dim]
+  float* std;         // [B][dim]
+  float* ess;         // [B]
+  int dim;
+  float eps;          // _posterior_stats' eps
+};
+
+// VBN._posterior_stats (vbn.py:495-503) of one row whose weights this thread holds in
+// registers (pdf[j0 + k], k < PER): the same float arithmetic and reduction tree as
+// vbn_posterior_stats_kernel, without reading the weights back.
+template <int PER>
+__device__ __forceinline__ void row_stats(const vbn_stats_out& so, const float (&pdf)[PER], int S, int j0,
+                                          int64_t row, float* red) {
+#pragma clang fp contract(off)
+  float w[PER];
+  float a = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const float v = pdf[k];
+    w[k] = (j0 + k < S && !(v != v || v == INFINITY || v == -INFINITY)) ? fmaxf(v, 0.f) : 0.f;
+    a += w[k];
+  }
+  const float denom = nw_block_sum(a, red);
+  const bool ok = denom > so.eps;
+  const float dn = fmaxf(denom, so.eps), uni = 1.0f / (float)max(1, S);
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (j0 + k < S) {
+      w[k] = ok ? w[k] / dn : uni;
+      q += w[k] * w[k];
+    }
+  }
+  const float sq = nw_block_sum(q, red);
+  if (threadIdx.x == 0) so.ess[row] = 1.0f / fmaxf(sq, so.eps);
+  const int D = so.dim;
+  const float* xr = so.x + row * (int64_t)S * D;
+  for (int d = 0; d < D; ++d) {
+    float m = 0.f;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (j0 + k < S) m += w[k] * xr[(int64_t)(j0 + k) * D + d];
+    const float mu = nw_block_sum(m, red);
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (j0 + k < S) {
+        const float c = xr[(int64_t)(j0 + k) * D + d] - mu;
+        v += w[k] * (c * c);
+      }
+    }
+    const float var = nw_block_sum(v, red);
+    if (threadIdx.x == 0) {
+      so.mean[row * D + d] = mu;
+      so.std[row * D + d] = sqrtf(fmaxf(var, 0.f));
+    }
+  }
+}
+
 // run_if (ABI v11): when non-NULL and *run_if == 0 the launch writes nothing (the predicated
 // fallback normalisation).  flag: when non-NULL, set to 1 (atomic OR) by every query whose
 // ESS < ess_thr (a NaN ESS never sets it; importance_sampling.py:85-86); the caller zeroes it.
@@ -100,7 +174,7 @@ __global__ void __launch_bounds__(NW_THREADS) vbn_normalize_reg_kernel(const flo
                                                                       float* __restrict__ w, float* __restrict__ ess,
                                                                       int S, int normalize, float eps,
                                                                       const int32_t* run_if, int32_t* flag,
-                                                                      float ess_thr) {
+                                                                      float ess_thr, const vbn_stats_out so) {
   if (run_if && *run_if == 0) return;
   __shared__ float red[NW_THREADS / WAVE];
   __shared__ int nan_flag;
@@ -138,17 +212,20 @@ __global__ void __launch_bounds__(NW_THREADS) vbn_normalize_reg_kernel(const flo
   for (int k = 1; k < NW_THREADS / WAVE; ++k) m = fmaxf(m, red[k]);
   const bool row_nan = nan_flag != 0;
   __syncthreads();
+  float e[PER];
   if (!normalize) {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
+      e[k] = 0.f;
       if (j0 + k < S) {
-        const float e = expf(v[k] - m);               // all -inf row: exp(NaN) stays NaN
-        y[j0 + k] = row_nan ? NAN : (e != e ? e : fmaxf(e, eps));
+        const float t = expf(v[k] - m);               // all -inf row: exp(NaN) stays NaN
+        e[k] = row_nan ? NAN : (t != t ? t : fmaxf(t, eps));
+        y[j0 + k] = e[k];
       }
     }
+    if (so.x) row_stats<PER>(so, e, S, j0, row, red);
     return;
   }
-  float e[PER];
   float sum = 0.f;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
@@ -187,6 +264,7 @@ __global__ void __launch_bounds__(NW_THREADS) vbn_normalize_reg_kernel(const flo
     if (ess) ess[row] = es;
     if (flag && es < ess_thr) atomicOr(flag, 1);
   }
+  if (so.x) row_stats<PER>(so, e, S, j0, row, red);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -393,6 +471,53 @@ __global__ void __launch_bounds__(RB_THREADS) vbn_posterior_stats_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// the same summary finished from the MCM walk's epilogue partials (vbn_walk_args.stats_part,
+// vbn_walk_impl.h stats_partials): one thread per query merges its S / 64 wave rows in float64
+// (Chan et al.'s pairwise update: M2 = sum_k M2_k + W_k (m_k - mean)^2).  Uniform weights where
+// W <= eps (vbn.py:497-498): the unweighted (m_u, M2_u) rows, 64 particles each.
+// ------------------------------------------------------------------------------------------
+#define SM_THREADS 64
+__global__ void __launch_bounds__(SM_THREADS) vbn_stats_merge_kernel(
+    const double* __restrict__ part, int64_t n_queries, int n_parts, int D, float eps, float* __restrict__ mean,
+    float* __restrict__ stdv, float* __restrict__ ess) {
+  const int64_t b = (int64_t)blockIdx.x * SM_THREADS + threadIdx.x;
+  if (b >= n_queries) return;
+  const int stride = 2 + 4 * D;
+  const double* r = part + b * n_parts * (int64_t)stride;
+  double W = 0.0, Q = 0.0;
+  for (int k = 0; k < n_parts; ++k) {
+    W += r[(int64_t)k * stride];
+    Q += r[(int64_t)k * stride + 1];
+  }
+  const bool ok = W > (double)eps;
+  const double S = 64.0 * n_parts;
+  if (ok) {
+    ess[b] = 1.0f / fmaxf((float)(Q / (W * W)), eps);
+  } else {
+    const float uni = 1.0f / (float)max(1, 64 * n_parts);
+    ess[b] = 1.0f / fmaxf((float)(64 * n_parts) * (uni * uni), eps);
+  }
+  for (int d = 0; d < D; ++d) {
+    const int o = 2 + 4 * d + (ok ? 0 : 2);
+    double m = 0.0;
+    for (int k = 0; k < n_parts; ++k) {
+      const double wk = ok ? r[(int64_t)k * stride] : 64.0;
+      m += wk * r[(int64_t)k * stride + o];
+    }
+    m /= ok ? W : S;
+    double m2 = 0.0;
+    for (int k = 0; k < n_parts; ++k) {
+      const double wk = ok ? r[(int64_t)k * stride] : 64.0;
+      const double c = r[(int64_t)k * stride + o] - m;
+      m2 += r[(int64_t)k * stride + o + 1] + wk * (c * c);   // 0 * NaN keeps a NaN sample's NaN
+    }
+    const double var = m2 / (ok ? W : S);
+    mean[b * D + d] = (float)m;
+    stdv[b * D + d] = sqrtf(fmaxf((float)var, 0.f));
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // discrete weighted histogram of a target's samples (benchmarking/models/vbn.py:202-242,
 // _estimate_discrete_posterior[_batch]): one lane per query walks its S (sample, weight) pairs
 // in order -- the reference's float64 running sums, so the bins are bit-identical -- skipping
@@ -513,6 +638,10 @@ static int walk_shape(const vbn_walk_args* a, walk_launch* out) {
                        a->wave_particles == 32 || (a->state && a->state_flags != 4)))
     return fail(VBN_E_ARGS, "vbn_hip_walk: precomp_q (per-query quantities) needs a lean full-wave walk "
                             "with n_samples a multiple of 64");
+  if (a->stats_part && (a->mode != VBN_MODE_MCM || (a->n_samples % WAVE) != 0 || a->wave_particles == 32 ||
+                        !a->out_cols || a->n_out_cols <= 0 || a->n_out_cols > 15))
+    return fail(VBN_E_ARGS, "vbn_hip_walk: stats_part (fused posterior summary) needs an MCM full-wave walk "
+                            "with n_samples a multiple of 64 and 1..15 output columns");
   if (a->wbuf_floats < 0 || (a->wbuf_floats % WBLK_CHUNK) != 0)
     return fail(VBN_E_ARGS, "vbn_hip_walk: wbuf_floats must be a non-negative multiple of 256");
   if (a->wave_particles != 0 && a->wave_particles != 32 && a->wave_particles != WAVE)
@@ -786,28 +915,60 @@ extern "C" int vbn_hip_rb_epilogue(const float* log_w, const float* params, int6
   return 0;
 }
 
-extern "C" int vbn_hip_normalize_weights_ex(const float* log_w, float* w, float* ess, int64_t n_queries,
-                                            int32_t n_samples, int32_t normalize, float eps, const int32_t* run_if,
-                                            int32_t* flag, float ess_thr, void* stream) {
+static int normalize_launch(const float* log_w, float* w, float* ess, int64_t n_queries, int32_t n_samples,
+                            int32_t normalize, float eps, const int32_t* run_if, int32_t* flag, float ess_thr,
+                            const vbn_stats_out& so, void* stream) {
   if (!log_w || !w || n_queries <= 0 || n_samples <= 0 || (flag && !normalize))
     return fail(VBN_E_ARGS, "vbn_hip_normalize_weights: bad arguments");
   // rows of up to 4096 weights stay in registers (vbn_normalize_reg_kernel; 16-byte loads need
   // 16-byte aligned rows); longer rows stream three times through the strided form
   const bool al = ((uintptr_t)log_w & 15) == 0 && ((uintptr_t)w & 15) == 0;
+  if (so.x && !(al && n_samples <= NW_THREADS * 16))
+    return fail(VBN_E_ARGS, "vbn_hip_normalize_weights_stats: needs n_samples <= 4096 and 16-byte aligned rows");
   const dim3 g((unsigned)n_queries), blk(NW_THREADS);
   hipStream_t st = (hipStream_t)stream;
   if (al && n_samples <= NW_THREADS * 4)
     hipLaunchKernelGGL(vbn_normalize_reg_kernel<4>, g, blk, 0, st, log_w, w, ess, n_samples, normalize, eps, run_if,
-                       flag, ess_thr);
+                       flag, ess_thr, so);
   else if (al && n_samples <= NW_THREADS * 8)
     hipLaunchKernelGGL(vbn_normalize_reg_kernel<8>, g, blk, 0, st, log_w, w, ess, n_samples, normalize, eps, run_if,
-                       flag, ess_thr);
+                       flag, ess_thr, so);
   else if (al && n_samples <= NW_THREADS * 16)
     hipLaunchKernelGGL(vbn_normalize_reg_kernel<16>, g, blk, 0, st, log_w, w, ess, n_samples, normalize, eps, run_if,
-                       flag, ess_thr);
+                       flag, ess_thr, so);
   else
     hipLaunchKernelGGL(vbn_normalize_kernel, g, blk, 0, st, log_w, w, ess, n_samples, normalize, eps, run_if, flag,
                        ess_thr);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  return 0;
+}
+
+extern "C" int vbn_hip_normalize_weights_ex(const float* log_w, float* w, float* ess, int64_t n_queries,
+                                            int32_t n_samples, int32_t normalize, float eps, const int32_t* run_if,
+                                            int32_t* flag, float ess_thr, void* stream) {
+  const vbn_stats_out none{nullptr, nullptr, nullptr, nullptr, 0, 0.f};
+  return normalize_launch(log_w, w, ess, n_queries, n_samples, normalize, eps, run_if, flag, ess_thr, none, stream);
+}
+
+extern "C" int vbn_hip_normalize_weights_stats(const float* log_w, float* w, float* ess, int64_t n_queries,
+                                               int32_t n_samples, int32_t normalize, float eps,
+                                               const int32_t* run_if, int32_t* flag, float ess_thr, const float* x,
+                                               int32_t dim, float stats_eps, float* mean, float* std,
+                                               float* stats_ess, void* stream) {
+  if (!x || !mean || !std || !stats_ess || dim <= 0)
+    return fail(VBN_E_ARGS, "vbn_hip_normalize_weights_stats: bad arguments");
+  const vbn_stats_out so{x, mean, std, stats_ess, dim, stats_eps};
+  return normalize_launch(log_w, w, ess, n_queries, n_samples, normalize, eps, run_if, flag, ess_thr, so, stream);
+}
+
+extern "C" int vbn_hip_posterior_stats_merge(const double* part, int64_t n_queries, int32_t n_parts, int32_t dim,
+                                             float eps, float* mean, float* std, float* ess, void* stream) {
+  if (!part || !mean || !std || !ess || n_queries <= 0 || n_parts <= 0 || dim <= 0 || dim > 15)
+    return fail(VBN_E_ARGS, "vbn_hip_posterior_stats_merge: bad arguments");
+  const int64_t blocks = (n_queries + SM_THREADS - 1) / SM_THREADS;
+  hipLaunchKernelGGL(vbn_stats_merge_kernel, dim3((unsigned)blocks), dim3(SM_THREADS), 0, (hipStream_t)stream, part,
+                     n_queries, n_parts, dim, eps, mean, std, ess);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   return 0;

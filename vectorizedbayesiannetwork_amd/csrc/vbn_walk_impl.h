@@ -2192,6 +2192,47 @@ __device__ __forceinline__ void step_barrier() {
   __syncthreads();
 }
 
+// (ABI v13) Posterior-summary partials of VBN._posterior_stats (vbn.py:495-503) fused into an
+// MCM walk's epilogue: the wave's 64 particles all belong to query L.b (n_samples % 64 == 0), so
+// it reduces their weights w = pdf (nan / inf -> 0, clamped >= 0) and target values in float64
+// with xor butterflies (every lane ends with the same sums) and lane 0 writes one row of
+// vbn_walk_args.stats_part: [W, Q, per output column: m_w, M2_w, m_u, M2_u] (two-pass inside the
+// wave: the mean first, then the centred second moment around it).  A zero-weight wave keeps
+// m_w = sum w x (0, or NaN when a sample is NaN as in the reference's 0 * NaN).
+// vbn_hip_posterior_stats_merge combines a query's S / 64 rows.
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ void stats_partials(const vbn_walk_args& A, const Lane& L, float pdf) {
+  const int D = A.n_out_cols;
+  const double w = (pdf != pdf || pdf == INFINITY || pdf == -INFINITY) ? 0.0 : (double)fmaxf(pdf, 0.f);
+  const double W = wave_sum_f64(w), Q = wave_sum_f64(w * w);
+  const int stride = 2 + 4 * D;
+  double* row = A.stats_part + ((int64_t)L.b * (A.n_samples >> 6) + (L.s >> 6)) * stride;
+  if (L.lane == 0) {
+    row[0] = W;
+    row[1] = Q;
+  }
+  for (int d = 0; d < D; ++d) {
+    const double x = (double)vread(L, A.out_cols[d]);
+    const double sx = wave_sum_f64(w * x);
+    const double mw = W > 0.0 ? sx / W : sx;
+    const double cw = x - mw;
+    const double m2w = wave_sum_f64(w * (cw * cw));
+    const double mu = wave_sum_f64(x) * (1.0 / 64.0);
+    const double cu = x - mu;
+    const double m2u = wave_sum_f64(cu * cu);
+    if (L.lane == 0) {
+      row[2 + 4 * d] = mw;
+      row[3 + 4 * d] = m2w;
+      row[4 + 4 * d] = mu;
+      row[5 + 4 * d] = m2u;
+    }
+  }
+}
+
 // The walk.  A workgroup = nw (1, 2 or 4; blockDim.x / 64) waves, each owning 64 consecutive
 // particles with its own LDS value slots; the waves walk the same step table in lockstep (one
 // barrier per step) and share two LDS weight buffers: while step i runs on buffer i & 1, step
@@ -2284,6 +2325,7 @@ vbn_walk_kernel(const vbn_walk_args A, const float* __restrict__ params, const v
     for (int k = 0; k < A.n_out_cols; ++k)
       A.out_x[L.p * A.n_out_cols + k] = vread(L, A.out_cols[k]);
   }
+  if (A.stats_part && A.mode == VBN_MODE_MCM && L.wq && !L.mirror) stats_partials(A, L, __expf(lp));
 }
 
 // Instantiated kind sets: bits 0-4 the CPD kinds walked, bit 5 non-relu activations, bit 6 the

@@ -173,6 +173,7 @@ __device__ __forceinline__ void vbn_walk_plan_general(const vbn_walk_args& A, co
   if (A.out_x) {
     for (int k = 0; k < A.n_out_cols; ++k) A.out_x[L.p * A.n_out_cols + k] = vread(L, A.out_cols[k]);
   }
+  if (A.stats_part && A.mode == VBN_MODE_MCM && L.wq && !L.mirror) stats_partials(A, L, __expf(lp));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -294,6 +295,7 @@ __device__ __forceinline__ void vbn_walk_plan_body(const vbn_walk_args& A, const
     if (A.out_x) {
       for (int k = 0; k < A.n_out_cols; ++k) A.out_x[L.p * A.n_out_cols + k] = vread(L, A.out_cols[k]);
     }
+    if (A.stats_part && A.mode == VBN_MODE_MCM && L.wq) stats_partials(A, L, __expf(lp));
   } else {
 #ifdef VBN_PLAN_CHAIN_WAVES
     vbn_walk_plan_chains<KM>(A, params);

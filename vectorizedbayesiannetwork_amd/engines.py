@@ -341,13 +341,16 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
              seed: int, offset: int = 0, q_base: int = 0, noise=None,
              fixed_per_particle: bool = False, state: Optional[torch.Tensor] = None, state_flags: int = 0,
              step_begin: int = 0, step_end: int = -1, plan_jit: int = 1, run_if: Optional[torch.Tensor] = None,
-             out_x: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+             out_x: Optional[torch.Tensor] = None, stats_part: Optional[torch.Tensor] = None
+             ) -> Tuple[torch.Tensor, torch.Tensor]:
     """One launch of the particle walk; returns (lp [b,n] or empty, x [b,n,n_out_cols]).
     ``state``/``state_flags``/``step_begin``/``step_end``: one segment of a split walk;
     ``plan_jit``: ops.walk (0 interpreter, 1 plan-specialised for large lean launches, 2 always);
     ``run_if``: device int32 [1] predicating the launch (the plain plan, no pre-passes: their
     outputs are bit-identical; nothing runs and nothing is written when it holds 0); ``out_x``: samples written into this [b, n, n_out_cols]
-    tensor (a predicated launch that does not run leaves it as it was)."""
+    tensor (a predicated launch that does not run leaves it as it was); ``stats_part``: an MCM
+    walk's fused posterior-summary partials (float64 [b * n/64, 2 + 4 n_out_cols],
+    ops.posterior_stats_merge)."""
     n_out_cols = int(plan.out_cols.numel()) if plan.out_nodes else 0
     noise_b = 1
     if isinstance(noise, dict):
@@ -433,14 +436,21 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
             b1 = min(b, b0 + step)
             fx = fixed[b0:b1] if fixed.shape[0] == b else fixed
             a = args[:3] + (fx,) + args[4:6] + (b1 - b0,) + args[7:17] + (q_base + b0,) + args[18:]
-            l, x = ops.walk(*a, plan.wbuf, plan_jit, precomp,
-                            precomp_q[b0:b1] if precomp_q is not None else None)
+            pq = precomp_q[b0:b1] if precomp_q is not None else None
+            if stats_part is None:
+                l, x = ops.walk(*a, plan.wbuf, plan_jit, precomp, pq)
+            else:
+                rows = stats_part.shape[0] // b
+                l, x = ops.walk_ex(*a, plan.wbuf, plan_jit, precomp, pq,
+                                   stats_part=stats_part[b0 * rows:b1 * rows])
             lps.append(l.view(b1 - b0, n) if plan.mode != MODE_SAMPLE else l)
             xss.append(x.view(b1 - b0, n, -1) if n_out_cols else x)
         lp = torch.cat(lps) if plan.mode != MODE_SAMPLE else lps[0]
         x = torch.cat(xss) if n_out_cols else xss[0]
-    elif state is None and run_if is None and out_x is None:
+    elif state is None and run_if is None and out_x is None and stats_part is None:
         lp, x = ops.walk(*args, plan.wbuf, plan_jit, precomp, precomp_q)
+    elif state is None and run_if is None and out_x is None:
+        lp, x = ops.walk_ex(*args, plan.wbuf, plan_jit, precomp, precomp_q, stats_part=stats_part)
     elif state is None:
         lp, x = ops.walk_ex(*args, plan.wbuf, plan_jit, precomp, precomp_q, run_if=run_if,
                             out_x=None if out_x is None else out_x.view(b * n, n_out_cols))
@@ -451,6 +461,18 @@ def run_walk(pk: PackedModel, plan: QueryPlan, fixed: torch.Tensor, b: int, n: i
     if n_out_cols:
         x = x.view(b, n, n_out_cols)
     return lp, x
+
+
+def _stats_request(kwargs, xs: torch.Tensor) -> Optional[dict]:
+    """The caller's fused posterior-summary request (``_stats``: a dict with "eps", filled with
+    "mean" / "std" / "ess"; VBN.infer_relative) as normalize_weights_ex's ``stats`` argument, or
+    None when the normalisation cannot fuse it (S > 4096: the caller runs the separate pass)."""
+    stats = kwargs.get("_stats")
+    if stats is None or xs.dim() != 3 or xs.shape[1] > 4096 or xs.shape[2] < 1:
+        return None
+    stats["x"] = xs
+    stats.setdefault("eps", 1e-12)
+    return stats
 
 
 class _EngineBase:
@@ -522,8 +544,18 @@ class MonteCarloMarginalization(_EngineBase):
                          shared_roots=True, mode=MODE_MCM, skip=[x for x in model.topo if x not in keep])
             b_eff = b
         fx = _fixed_buffer(plan, vals, b_eff, dev)
+        stats = kwargs.get("_stats")
+        d = int(plan.out_cols.numel())
+        part = None
+        if stats is not None and n % 64 == 0 and 1 <= d <= 15:
+            # VBN._posterior_stats fused into the walk's epilogue (vbn_walk_args.stats_part)
+            rows, stride = ops.stats_part_rows(b_eff, n, d)
+            part = torch.empty(rows, stride, device=dev, dtype=torch.float64)
         pdf, xs = run_walk(pk, plan, fx, b_eff, n, seed=self._seed(kwargs), q_base=self.q_base,
-                           noise=kwargs.get("_noise"), plan_jit=self.plan_jit)
+                           noise=kwargs.get("_noise"), plan_jit=self.plan_jit, stats_part=part)
+        if part is not None:
+            stats["mean"], stats["std"], stats["ess"] = ops.posterior_stats_merge(part, b_eff, n, d,
+                                                                                   stats.get("eps", 1e-12))
         return pdf, xs
 
 
@@ -578,17 +610,24 @@ class LikelihoodWeighting(_EngineBase):
         eps = float(kwargs.get("eps", self.eps))
         log_w, xs = self._walk(vbn, query, n, clamp=True, shared_roots=True, kwargs=kwargs,
                                offset=int(kwargs.get("_offset", 0)), noise=kwargs.get("_noise"))
+        stats = _stats_request(kwargs, xs)
+        if stats is not None:
+            # VBN._posterior_stats fused into the normalisation (vbn_hip_normalize_weights_stats)
+            w, _, _ = ops.normalize_weights_ex(log_w, normalize, eps, stats=stats)
+            return w, xs
         w, _ = ops.normalize_weights(log_w, normalize, eps)
         return w, xs
 
     def infer_into(self, vbn, query, n: int, *, seed: int, offset: int, run_if: torch.Tensor,
-                   w_out: torch.Tensor, x_out: torch.Tensor, noise=None, fixed_from=None) -> None:
+                   w_out: torch.Tensor, x_out: torch.Tensor, noise=None, fixed_from=None, stats=None) -> None:
         """The whole LW call predicated on the device flag ``run_if``: walk and normalisation
         write their weights / samples into ``w_out`` / ``x_out`` when it holds 1 and launch as
-        no-ops otherwise (importance sampling's fallback without a host sync)."""
+        no-ops otherwise (importance sampling's fallback without a host sync); ``stats``: the
+        fused posterior summary's outputs, overwritten likewise."""
         log_w, _ = self._walk(vbn, query, n, clamp=True, shared_roots=True, kwargs={"_seed_value": seed},
                               offset=offset, noise=noise, run_if=run_if, out_x=x_out, fixed_from=fixed_from)
-        ops.normalize_weights_ex(log_w, self.normalize, self.eps, run_if=run_if, w_out=w_out)
+        ops.normalize_weights_ex(log_w, self.normalize, self.eps, run_if=run_if, w_out=w_out,
+                                 stats=None if stats is None else dict(stats, x=x_out))
 
 
 @register_inference("importance_sampling")
@@ -634,7 +673,8 @@ class ImportanceSampling(LikelihoodWeighting):
                                kwargs={**kwargs, "_seed_value": seed}, noise=kwargs.get("_noise"))
         # softmax + ESS, and the fallback decision (any ESS < threshold) on the device
         thr = max(1.0, self.ess_threshold * float(n))
-        w, ess, flag = ops.normalize_weights_ex(log_w, True, 0.0, ess_thr=thr)
+        stats = _stats_request(kwargs, xs)
+        w, ess, flag = ops.normalize_weights_ex(log_w, True, 0.0, ess_thr=thr, stats=stats)
         self._last_ess = ess
         reduce = kwargs.get("_reduce_flag")          # multi-GPU: batch-global decision
         if reduce is not None:
@@ -644,7 +684,8 @@ class ImportanceSampling(LikelihoodWeighting):
         # host never waits for the decision (the reference syncs here)
         self._lw.q_base = self.q_base
         self._lw.infer_into(vbn, query, n, seed=seed, offset=1, run_if=flag, w_out=w, x_out=xs,
-                            noise=kwargs.get("_noise_fallback"), fixed_from=self._last_fixed)
+                            noise=kwargs.get("_noise_fallback"), fixed_from=self._last_fixed,
+                            stats=None if stats is None else {k: stats[k] for k in ("mean", "std", "ess", "eps")})
         self._fallback_flag, self._fallback_bool = flag, None
         return w, xs
 

@@ -21,7 +21,7 @@ import torch
 from torch import Tensor
 
 from . import _lib
-from .plan import MODE_GIBBS, S_WBLK_LEN, STEP_INTS
+from .plan import MODE_GIBBS, MODE_MCM, S_WBLK_LEN, STEP_INTS
 
 __all__ = ["walk", "walk_segment", "normalize_weights", "rb_epilogue", "resample", "posterior_stats"]
 
@@ -60,10 +60,13 @@ def walk(steps: Tensor, in_cols: Tensor, params: Tensor, fixed: Tensor, noise: O
 
 def walk_ex(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out, fixed_ld,
             fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed, offset, want_lp,
-            kind_mask=63, wbuf=0, plan_jit=1, precomp=None, precomp_q=None, *, run_if=None, out_x=None):
+            kind_mask=63, wbuf=0, plan_jit=1, precomp=None, precomp_q=None, *, run_if=None, out_x=None,
+            stats_part=None):
     """:func:`walk` as a plain launch, plus ``run_if`` (device int32 [1]: the launch does
-    nothing when it holds 0, vbn_walk_args.run_if) and ``out_x`` (write the samples into this
-    [B*S, n_out_cols] tensor; a predicated launch that does not run leaves it untouched)."""
+    nothing when it holds 0, vbn_walk_args.run_if), ``out_x`` (write the samples into this
+    [B*S, n_out_cols] tensor; a predicated launch that does not run leaves it untouched) and
+    ``stats_part`` (float64 [B * S/64, 2 + 4 n_out_cols]: the MCM walk's fused posterior-summary
+    partials, vbn_walk_args.stats_part; :func:`posterior_stats_merge` finishes them)."""
     for name, t, rows, attr in (("precomp", precomp, n_samples, "_vbn_precomp_stride"),
                                 ("precomp_q", precomp_q, n_queries, "_vbn_precomp_q_stride")):
         need = getattr(steps, attr, None)
@@ -83,7 +86,7 @@ def walk_ex(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples
     return _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots,
                         max_out, fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode,
                         q_base, seed, offset, want_lp, kind_mask, precomp, 4 if precomp is not None else 0,
-                        0, -1, wbuf, plan_jit, precomp_q, run_if=run_if, out_x=out_x)
+                        0, -1, wbuf, plan_jit, precomp_q, run_if=run_if, out_x=out_x, stats_part=stats_part)
 
 
 @torch.library.custom_op("vbn_hip::walk_segment", mutates_args=("state",))
@@ -124,7 +127,7 @@ def _check_wbuf(op: str, steps: Tensor, begin: int, end: int, wbuf: int) -> None
 def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_samples, n_slots, max_out,
                  fixed_ld, fixed_per_particle, noise_b, n_noise, dmax, n_out_cols, mode, q_base, seed,
                  offset, want_lp, kind_mask, state, state_flags, step_begin, step_end, wbuf, plan_jit=0,
-                 precomp_q=None, run_if=None, out_x=None):
+                 precomp_q=None, run_if=None, out_x=None, stats_part=None):
     device = params.device
     if device.type != "cuda":
         raise RuntimeError("vbn_hip::walk runs on the GPU only (no CPU fallback); "
@@ -165,6 +168,12 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
         x = out_x
     if run_if is not None:
         _check_dev("run_if", run_if, torch.int32, device)
+    if stats_part is not None:
+        _check_dev("stats_part", stats_part, torch.float64, device)
+        rows, stride = stats_part_rows(n_queries, n_samples, n_out_cols)
+        if mode != MODE_MCM or n_samples % 64 or not 1 <= n_out_cols <= 15 or stats_part.numel() != rows * stride:
+            raise ValueError("vbn_hip::walk: stats_part needs an MCM walk with n_samples % 64 == 0, 1..15 output "
+                             f"columns and [{rows}, {stride}] float64 partials")
     a = _lib.VbnWalkArgs()
     a.steps = steps.data_ptr() + step_begin * STEP_INTS * 4 if step_end > step_begin else None
     a.in_cols = _ptr(in_cols)
@@ -181,6 +190,7 @@ def _walk_launch(steps, in_cols, params, fixed, noise, out_cols, n_queries, n_sa
     a.state_flags = int(state_flags)
     a.precomp_q = _ptr(precomp_q)
     a.run_if = _ptr(run_if)
+    a.stats_part = _ptr(stats_part)
     a.n_slots = n_slots
     a.max_out = max_out
     a.fixed_ld = fixed_ld
@@ -422,12 +432,16 @@ def _flag_slot(device: torch.device) -> Tensor:
 
 def normalize_weights_ex(log_w: Tensor, normalize: bool, eps: float, *, ess_thr: Optional[float] = None,
                          run_if: Optional[Tensor] = None, w_out: Optional[Tensor] = None,
-                         ess_out: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
+                         ess_out: Optional[Tensor] = None, stats: Optional[dict] = None
+                         ) -> Tuple[Tensor, Tensor, Optional[Tensor]]:
     """The normalisation kernel (vbn_hip_normalize_weights_ex) as a plain launch: ``ess_thr``
     returns a device int32 [1] flag, 1 when some query's ESS < ess_thr (importance_sampling.py
     :85-86, decided without a host sync); ``run_if`` (device int32 [1]) predicates the launch;
     ``w_out`` / ``ess_out``: write into these instead of fresh tensors (predicated launches
-    leave them untouched when *run_if == 0)."""
+    leave them untouched when *run_if == 0).  ``stats``: {"x": samples [B,S,D], "eps": float,
+    and optionally "mean" / "std" / "ess" output tensors}: VBN._posterior_stats of the weights
+    written, fused into the same pass (vbn_hip_normalize_weights_stats, S <= 4096); the dict
+    gets "mean" [B,D], "std" [B,D], "ess" [B]."""
     if log_w.device.type != "cuda" or log_w.dtype != torch.float32 or log_w.dim() != 2:
         raise ValueError("vbn_hip::normalize_weights: log_w must be a float32 [B,S] GPU tensor")
     log_w = log_w.contiguous()
@@ -447,6 +461,25 @@ def normalize_weights_ex(log_w: Tensor, normalize: bool, eps: float, *, ess_thr:
             raise ValueError("vbn_hip::normalize_weights: the ESS flag needs normalize=True")
         flag = _flag_slot(log_w.device)
     lib = _lib.load()
+    if stats is not None:
+        x = stats["x"]
+        _check_dev("stats x", x, torch.float32, log_w.device)
+        if x.dim() != 3 or tuple(x.shape[:2]) != (b, s) or s > 4096:
+            raise ValueError(f"vbn_hip::normalize_weights: stats x must be [{b}, {s}, D] with S <= 4096")
+        d = int(x.shape[2])
+        for name, shape in (("mean", (b, d)), ("std", (b, d)), ("ess", (b,))):
+            t = stats.get(name)
+            if t is None:
+                stats[name] = torch.empty(shape, device=log_w.device, dtype=torch.float32)
+            elif t.dtype != torch.float32 or tuple(t.shape) != shape or not t.is_contiguous():
+                raise ValueError(f"vbn_hip::normalize_weights: stats {name} must be a contiguous float32 {shape}")
+        with torch.cuda.device(log_w.device):
+            _lib.check(lib.vbn_hip_normalize_weights_stats(
+                _ptr(log_w), _ptr(w), _ptr(ess) if normalize else None, b, s, int(normalize), float(eps),
+                _ptr(run_if), _ptr(flag), float(ess_thr or 0.0), _ptr(x), d, float(stats.get("eps", 1e-12)),
+                _ptr(stats["mean"]), _ptr(stats["std"]), _ptr(stats["ess"]),
+                ctypes.c_void_p(_stream_handle(log_w.device))), "vbn_hip_normalize_weights_stats")
+        return w, ess, flag
     with torch.cuda.device(log_w.device):
         _lib.check(lib.vbn_hip_normalize_weights_ex(
             _ptr(log_w), _ptr(w), _ptr(ess) if normalize else None, b, s, int(normalize), float(eps),
@@ -550,6 +583,31 @@ def posterior_stats(pdf: Tensor, samples: Tensor, eps: float) -> Tuple[Tensor, T
 def _posterior_stats_fake(pdf, samples, eps):
     b, d = pdf.shape[0], samples.shape[2]
     return pdf.new_empty(b, d), pdf.new_empty(b, d), pdf.new_empty(b)
+
+
+def stats_part_rows(n_queries: int, n_samples: int, dim: int) -> Tuple[int, int]:
+    """(rows, doubles per row) of a walk's fused posterior-summary partials
+    (vbn_walk_args.stats_part): one row per 64-particle wave."""
+    return n_queries * (n_samples // 64), 2 + 4 * dim
+
+
+def posterior_stats_merge(part: Tensor, n_queries: int, n_samples: int, dim: int, eps: float
+                          ) -> Tuple[Tensor, Tensor, Tensor]:
+    """Finish VBN._posterior_stats (vbn.py:483-504) from an MCM walk's epilogue partials
+    (vbn_hip_posterior_stats_merge): (mean [B,D], std [B,D], ess [B])."""
+    rows, stride = stats_part_rows(n_queries, n_samples, dim)
+    _check_dev("stats_part", part, torch.float64, part.device)
+    if part.numel() != rows * stride:
+        raise ValueError(f"vbn_hip::posterior_stats_merge: part has {part.numel()} values, needs {rows * stride}")
+    mean = torch.empty(n_queries, dim, device=part.device, dtype=torch.float32)
+    std = torch.empty_like(mean)
+    ess = torch.empty(n_queries, device=part.device, dtype=torch.float32)
+    lib = _lib.load()
+    with torch.cuda.device(part.device):
+        _lib.check(lib.vbn_hip_posterior_stats_merge(
+            _ptr(part), n_queries, n_samples // 64, dim, float(eps), _ptr(mean), _ptr(std), _ptr(ess),
+            ctypes.c_void_p(_stream_handle(part.device))), "vbn_hip_posterior_stats_merge")
+    return mean, std, ess
 
 
 @torch.library.custom_op("vbn_hip::discrete_posterior", mutates_args=())
