@@ -31,7 +31,8 @@ def _check(st, pdf, xs, eps=1e-12):
     for k in ("mean", "std", "ess"):
         got = st[k].cpu()
         assert got.shape == ref[k].shape, k
-        torch.testing.assert_close(got.double(), ref[k], rtol=RTOL, atol=ATOL, equal_nan=True, msg=k)
+        torch.testing.assert_close(got.double(), ref[k], rtol=RTOL, atol=ATOL, equal_nan=True,
+                                   msg=lambda m, k=k: f"{k}: {m}")
 
 
 def _query(vbn, target, ev_nodes, b, seed=0):
@@ -150,6 +151,9 @@ def test_normalisation_summary_edge_rows(s):
         w, _, _ = ops.normalize_weights_ex(lw, normalize, 1e-12, stats=st)
         torch.cuda.synchronize()
         _check(st, w, x)
+        # the separate pass on the same rows (a NaN sample keeps its NaN std, as clamp_min does)
+        mean, std, ess = ops.posterior_stats(w, x, 1e-12)
+        _check({"mean": mean, "std": std, "ess": ess}, w, x)
 
 
 def test_infer_relative_takes_the_fused_forms():
@@ -165,7 +169,7 @@ def test_infer_relative_takes_the_fused_forms():
         qp, qs = b.infer_posterior(q)
         rp, rs = b.infer_posterior({"target": topo[0]})
         for stats, (p, s) in ((out["query_stats"], (qp, qs)), (out["reference_stats"], (rp, rs))):
-            ref = b._posterior_stats(p, s)
-            torch.testing.assert_close(stats["mean"].cpu(), ref["mean"].cpu(), rtol=RTOL, atol=ATOL)
-            torch.testing.assert_close(stats["std"].cpu(), ref["std"].cpu(), rtol=RTOL, atol=ATOL)
-            torch.testing.assert_close(stats["effective_sample_size"].cpu(), ref["ess"].cpu(), rtol=RTOL, atol=ATOL)
+            ref = b._posterior_stats(p, s)            # [1, ...] for the reference query: broadcast
+            for got, want in ((stats["mean"], ref["mean"]), (stats["std"], ref["std"]),
+                              (stats["effective_sample_size"], ref["ess"])):
+                torch.testing.assert_close(got.cpu(), want.expand_as(got).cpu(), rtol=RTOL, atol=ATOL)

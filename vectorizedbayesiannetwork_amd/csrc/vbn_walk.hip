@@ -25,6 +25,9 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// sqrt(var.clamp_min(0)) as torch computes it: clamp_min keeps a NaN (fmaxf would drop it)
+__device__ __forceinline__ float std_of_var(float v) { return sqrtf(v < 0.f ? 0.f : v); }
+
 // sum over the NW_THREADS threads of a workgroup (every thread gets the total)
 __device__ __forceinline__ float nw_block_sum(float v, float* red) {
   v = wave_sum(v);
@@ -94,7 +97,7 @@ __device__ __forceinline__ void row_stats(const vbn_stats_out& so, const float (
     const float var = nw_block_sum(v, red);
     if (threadIdx.x == 0) {
       so.mean[row * D + d] = mu;
-      so.std[row * D + d] = sqrtf(fmaxf(var, 0.f));
+      so.std[row * D + d] = std_of_var(var);
     }
   }
 }
@@ -465,7 +468,7 @@ __global__ void __launch_bounds__(RB_THREADS) vbn_posterior_stats_kernel(
     const float var = block_sum(v, red);
     if (tid == 0) {
       mean[b * D + d] = mu;
-      stdv[b * D + d] = sqrtf(fmaxf(var, 0.f));
+      stdv[b * D + d] = std_of_var(var);
     }
   }
 }
@@ -513,7 +516,7 @@ __global__ void __launch_bounds__(SM_THREADS) vbn_stats_merge_kernel(
     }
     const double var = m2 / (ok ? W : S);
     mean[b * D + d] = (float)m;
-    stdv[b * D + d] = sqrtf(fmaxf((float)var, 0.f));
+    stdv[b * D + d] = std_of_var((float)var);
   }
 }
 
