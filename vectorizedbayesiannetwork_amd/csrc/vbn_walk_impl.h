@@ -1518,10 +1518,25 @@ __device__ __forceinline__ void kde_b32_sums(const bf16x8* __restrict__ pa, int 
 // KDE_FFORM_MAX (no overflow: sums <= M 2^{|x'|^2}); otherwise the full form.
 #define KDE_FFORM_MAX 96.f
 
+// Sub-chunks (round 6; VBN_ABL_NOHALVES: A/B without).  A wave's scan lasts as long as its
+// slowest lane's, about half a chunk (the max over 64 lanes of the bidirectional walk).  Pass 1
+// therefore also keeps KDE_NSUB - 1 prefix sums per chunk (a private array: the LDS rows are
+// the occupancy budget -- 32 chunk rows instead cost 16 -> 12 waves per CU and ran slower), at
+// block boundaries kde_sub_blocks(cb32, k) (multiples of KDE_PF, about k / KDE_NSUB of the
+// chunk), and the scan covers the sub-chunk holding the threshold.  cfg4 plain plan, one box
+// (profiles/r06_bench/r06i_ab_sub.txt): 88.86 ms -> 81.82 (halves) / 81.87 (quarters).
+#ifndef KDE_NSUB
+#define KDE_NSUB 2
+#endif
+__device__ __forceinline__ int kde_sub_blocks(int cb32, int k) {
+  return ((cb32 * k) / KDE_NSUB) & ~(KDE_PF - 1);
+}
+
 // Pass 1 of a node with nf features over its KDE_CHUNKS chunks: chunk sums -> scr[chunk][lane]
 template <int KG, int PG>
 __device__ __forceinline__ double kde_pass1(const bf16x8* __restrict__ pa, int cb32, const Lane& L,
-                                            const int (&slots)[4], const float (&scl)[4], int nf, bool fform) {
+                                            const int (&slots)[4], const float (&scl)[4], int nf, bool fform,
+                                            float* __restrict__ hs = nullptr) {
   KdeB32<KG> o;
   kde_b32_ops<KG>(L, slots, scl, nf, fform, o);
   const int blast = KDE_CHUNKS * cb32 - 1;
@@ -1530,7 +1545,19 @@ __device__ __forceinline__ double kde_pass1(const bf16x8* __restrict__ pa, int c
   double tot = 0.0;
   for (int ch = 0; ch < KDE_CHUNKS; ++ch) {
     float s[2] = {0.f, 0.f};
-    kde_b32_sums<KG, PG>(pa, ch * cb32, ch * cb32 + cb32, blast, o, s, q);
+    if (hs) {                                         // the sub-chunk prefix sums on the way
+      int b = ch * cb32;
+#pragma unroll
+      for (int k = 1; k < KDE_NSUB; ++k) {
+        const int bk = ch * cb32 + kde_sub_blocks(cb32, k);
+        kde_b32_sums<KG, PG>(pa, b, bk, blast, o, s, q);
+        hs[ch * (KDE_NSUB - 1) + k - 1] = kde_reduce_tiles(s, L.lane);
+        b = bk;
+      }
+      kde_b32_sums<KG, PG>(pa, b, ch * cb32 + cb32, blast, o, s, q);
+    } else {
+      kde_b32_sums<KG, PG>(pa, ch * cb32, ch * cb32 + cb32, blast, o, s, q);
+    }
     const float cs = kde_reduce_tiles(s, L.lane);
     L.scr[ch * WAVE + L.lane] = cs;
     tot += (double)cs;
@@ -1701,6 +1728,12 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
     }
   }
   float shift = 0.f;                                  // sigma: the sums are of exp2(a' - sigma)
+  // pass 1 also keeps each chunk's first-half sum (a private array, kde_sub_blocks), so the
+  // scan covers the half holding the threshold: at most a quarter chunk instead of a half
+  bool halves = false;
+#ifndef VBN_ABL_NOHALVES
+  float hs[KDE_CHUNKS * (KDE_NSUB - 1)];
+#endif
   if (pre) {                                          // pass 1 of this sample / query, pre-pass
     if (st.flags & VBN_F_PRECOMP_Q) {
       const cfloat* q = precomp_qrow(A, st, L);
@@ -1729,16 +1762,23 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
     const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
     const bool fform = __all(-negsq <= KDE_FFORM_MAX);
     shift = fform ? 0.f : -negsq;
+#ifndef VBN_ABL_NOHALVES
+    float* hsp = (st.flags & VBN_F_PRE_OUT) ? nullptr : hs;
+    halves = hsp != nullptr;
+#else
+    float* hsp = nullptr;
+#endif
     if (nf == 1)
-      tot = kde_pass1<1, 1>(pa, cb >> 1, L, slots, scl, nf, fform);
+      tot = kde_pass1<1, 1>(pa, cb >> 1, L, slots, scl, nf, fform, hsp);
     else if (nf == 2 && fform)
-      tot = kde_pass1<1, 2>(pa, cb >> 1, L, slots, scl, nf, fform);
+      tot = kde_pass1<1, 2>(pa, cb >> 1, L, slots, scl, nf, fform, hsp);
     else
-      tot = kde_pass1<2, 2>(pa, cb >> 1, L, slots, scl, nf, fform);
+      tot = kde_pass1<2, 2>(pa, cb >> 1, L, slots, scl, nf, fform, hsp);
   }
   const int nfr = nf;                                 // replica form of the pass-1 elements
   const float xb0 = 2.f * xv[0], xb1 = 2.f * xv[1], xb2 = 2.f * xv[2];
   if (!pre && !(tot > 0.0)) {                         // every weight underflowed (or NaN parent)
+    halves = false;
     float amax = -INFINITY;
     for (int j = 0; j < M; ++j) amax = fmaxf(amax, kde_arg_rec(rec[j], xb0, xb1, xb2, 0.f, nfr));
     shift = amax;
@@ -1771,8 +1811,27 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   wave_sync();
   return min(j0, M - 1);
 #endif
-  const float rem = (float)(thr - cum);
-  const float csum = L.scr[ch * WAVE + lane];
+  float rem = (float)(thr - cum);
+  float csum = L.scr[ch * WAVE + lane];
+  int jlo = j0, jhi = j1;
+#ifndef VBN_ABL_NOHALVES
+  if (halves) {                                       // the sub-chunk holding thr
+    const double rd = thr - cum;
+    float plo = 0.f, phi = csum;
+    int klo = 0, khi = KDE_NSUB;
+#pragma unroll
+    for (int k = 1; k < KDE_NSUB; ++k) {
+      const float pk = hs[ch * (KDE_NSUB - 1) + k - 1];
+      if (rd >= (double)pk) { klo = k; plo = pk; }
+      else if (khi == KDE_NSUB) { khi = k; phi = pk; }
+    }
+    const int cb32 = cb >> 1;
+    jlo = klo ? min(M, j0 + 32 * kde_sub_blocks(cb32, klo)) : j0;
+    jhi = khi < KDE_NSUB ? min(M, j0 + 32 * kde_sub_blocks(cb32, khi)) : j1;
+    rem = (float)(rd - (double)plo);
+    csum = phi - plo;
+  }
+#endif
   const float4* __restrict__ rev = rec + (((M + 15) >> 4) * 16 + KDE_REC_TAIL);
   int idx;
   // the replica chain a' = 2 x'.y' - |y'|^2 per feature count, compile-time (kde_arg_rec with
@@ -1780,14 +1839,14 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   // (the shift enters the chain as its addend: -0 in the factored form, so the same values)
   const float nsh = -shift;
   if (nfr == 1)
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum,
+    idx = kde_scan(rec, rev, M, jlo, jhi, rem, csum,
                    [&](const float4 r) { return fmaf(r.y, -1.f, fmaf(r.x, xb0, nsh)); });
   else if (nfr == 2)
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, [&](const float4 r) {
+    idx = kde_scan(rec, rev, M, jlo, jhi, rem, csum, [&](const float4 r) {
       return fmaf(r.z, -1.f, fmaf(r.y, xb1, fmaf(r.x, xb0, nsh)));
     });
   else
-    idx = kde_scan(rec, rev, M, j0, j1, rem, csum, [&](const float4 r) {
+    idx = kde_scan(rec, rev, M, jlo, jhi, rem, csum, [&](const float4 r) {
       return fmaf(r.w, -1.f, fmaf(r.z, xb2, fmaf(r.y, xb1, fmaf(r.x, xb0, nsh))));
     });
   wave_sync();
