@@ -1662,7 +1662,7 @@ __device__ __forceinline__ int kde_scan(const float4* __restrict__ rec, const fl
 #define KDE_MT_HEAD 8         // header floats (plan.KDE_MT_HEADER)
 #define KDE_MT_GROUP 8        // chunks per group (plan.KDE_MT_GROUP)
 __device__ __forceinline__ int kde_index_moments(const float* __restrict__ T, float xb0, float ucat,
-                                                 const float4* __restrict__ rec, int M) {
+                                                 const float4* __restrict__ rec, int M, float& total) {
   const cfloat* H = CP(T);
   const float u_lo = H[0], inv_d = H[1], dlt = H[2];
   const int n_cells = __float_as_int(H[3]), nch = __float_as_int(H[4]), per = __float_as_int(H[5]);
@@ -1673,7 +1673,8 @@ __device__ __forceinline__ int kde_index_moments(const float* __restrict__ T, fl
   const int ng = (nch + KDE_MT_GROUP - 1) / KDE_MT_GROUP;
   const float4* __restrict__ row = reinterpret_cast<const float4*>(T + KDE_MT_HEAD) + (int)gr * (nch + ng + 1);
   auto poly = [&](const float4 c) { return fmaf(fmaf(fmaf(c.w, d, c.z), d, c.y), d, c.x); };
-  const double thr = (double)ucat * (double)poly(row[nch + ng]);
+  total = poly(row[nch + ng]);
+  const double thr = (double)ucat * (double)total;
   double cum = 0.0;
   float gs = 0.f;
   int g = ng - 1;
@@ -1706,8 +1707,11 @@ __device__ __forceinline__ int kde_index_moments(const float* __restrict__ T, fl
 // Pass 1 (MFMA): per-chunk weight sums -> scr[chunk][lane]; pass 2 (VALU replica): locate the
 // chunk holding u * total, scan it.  All-underflow particles (every weight 0) redo the sums on
 // VALU relative to their largest weight.
+// lsp (out): ln sum_j K_p(x, y_j) -- the node's own log-density denominator (kde.py:141-146), from
+// pass 1's total, ln(tot) + (sigma - |x'|^2) ln 2 in every form (factored, full, rescued,
+// precomputed, moment table); NaN when pass 1 gave no positive total
 __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_step& st, const Lane& L,
-                                              float ucat, float c_p) {
+                                              float ucat, float c_p, float& lsp) {
   const int M = st.k, nf = st.aux0, lane = L.lane;
   const int cb = kde_cb(M);
   int slots[4] = {0, 0, 0, 0};
@@ -1721,8 +1725,10 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
   const float4* __restrict__ rec = reinterpret_cast<const float4*>(L.P + st.reserved[3]) + 4;
   if (nf == 1 && KDE_MT(st) >= 0 && !(st.flags & (VBN_F_PRECOMP | VBN_F_PRE_OUT)) &&
       __all(-negsq <= KDE_FFORM_MAX)) {               // a one-feature node with a moment table
-    const int idx = kde_index_moments(L.P + KDE_MT(st), 2.f * xv[0], ucat, rec, M);
+    float mtot = 0.f;
+    const int idx = kde_index_moments(L.P + KDE_MT(st), 2.f * xv[0], ucat, rec, M, mtot);
     if (idx >= 0) {                                   // the whole wave took it
+      if (mtot > 0.f) lsp = __logf(mtot) + negsq * VBN_LN2_F;   // factored form (sigma 0)
       wave_sync();
       return idx;
     }
@@ -1792,6 +1798,7 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
       tot += (double)cs;
     }
   }
+  if (tot > 0.0) lsp = __logf((float)tot) + (shift + negsq) * VBN_LN2_F;
   if (st.flags & VBN_F_PRE_OUT) {                    // pre-pass: pass 1's result is the output
     for (int c = 0; c < KDE_CHUNKS; ++c) vwrite(L, st.out_col + c, L.scr[c * WAVE + lane]);
     vwrite(L, st.out_col + KDE_CHUNKS, shift);
@@ -1859,7 +1866,7 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
 // pack kq (parent features) and kqy (parent ++ target features, scales c_p / c_y).  Returns
 // false (nothing added) when a sum underflows; the caller then takes the shifted VALU path.
 __device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L, bool root, float c_p,
-                                              float c_y, float cy, float log_n, float& lp) {
+                                              float c_y, float cy, float log_n, float& lp, float lsp) {
   const int M = st.k, dp = st.aux0, D = st.out_dim, lane = L.lane;
   // the blocks holding points (a whole number of KDE_PF blocks), not the chunk-padded pack: the
   // blocks past them hold only weight-0 padding, whose +0 terms leave every sum unchanged
@@ -1877,6 +1884,18 @@ __device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L,
   const bool fform = __all(sq_y <= KDE_FFORM_MAX);
   const bf16x8* __restrict__ pay = reinterpret_cast<const bf16x8*>(L.P + st.reserved[2]) + lane;
   const float sy = kde_sums_nf(pay, nb32, L, slots, scl, ny, fform);
+  constexpr float LN2 = 0.69314718055994531f;
+#ifndef VBN_ABL_NOLSP
+  // a sampled node's denominator is its own pass 1's total (kde_index_mfma lsp): every lane of
+  // the wave has it, so the parent-feature pass is not run again (cfg4's target: M exps per
+  // particle)
+  if (!root && __all(lsp == lsp)) {
+    wave_sync();
+    if (!(sy > 0.f)) return false;
+    lp += ((__logf(sy) - (fform ? sq_y * LN2 : 0.f)) - lsp) + cy;
+    return true;
+  }
+#endif
   float sp = 1.f;
   if (!root) {
     const bf16x8* __restrict__ pa = reinterpret_cast<const bf16x8*>(L.P + st.reserved[1]) + lane;
@@ -1884,7 +1903,6 @@ __device__ __forceinline__ bool kde_logp_mfma(const vbn_step& st, const Lane& L,
   }
   wave_sync();
   if (!(sy > 0.f) || !(sp > 0.f)) return false;
-  constexpr float LN2 = 0.69314718055994531f;
   const float corr = fform ? (root ? sq_y : sq_y - sq_p) * LN2 : 0.f;
   lp += root ? ((__logf(sy) - corr) + cy - log_n) : (((__logf(sy) - __logf(sp)) - corr) + cy);
   return true;
@@ -1996,6 +2014,7 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
 #pragma unroll
   for (int i = 0; i < (DP > 0 ? DP : 0); ++i) pv[i] = vread(L, L.ic[st.in_off + i]);
 
+  float lsp = __int_as_float(0x7fc00000);            // the sampling pass's ln sum_j K_p (NaN: none)
   if (st.role == VBN_ROLE_LATENT) {
     const float ucat = draw_uniforms(A, st, 0, L).x;
     int idx;
@@ -2005,7 +2024,7 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
       idx = st.aux0 == 1 ? kde_index_valu<1>(A, st, L, ucat, c_p)
           : (st.aux0 == 2 ? kde_index_valu<2>(A, st, L, ucat, c_p) : kde_index_valu<3>(A, st, L, ucat, c_p));
     } else if (st.reserved[1] >= 0) {
-      idx = kde_index_mfma(A, st, L, ucat, c_p);
+      idx = kde_index_mfma(A, st, L, ucat, c_p, lsp);
       if (st.flags & VBN_F_PRE_OUT) return;            // pre-pass: sums written, no sample
     } else {
       // pass 1: per-chunk weight sums -> scr[chunk][lane]
@@ -2065,7 +2084,7 @@ __device__ __forceinline__ void step_kde_t(const vbn_walk_args& A, const vbn_ste
 
   if ((st.flags & VBN_F_LOGP) && st.reserved[2] >= 0 && (root || st.reserved[1] >= 0)) {
     wave_sync();
-    if (kde_logp_mfma(st, L, root, c_p, c_y, cy, log_n, lp)) return;
+    if (kde_logp_mfma(st, L, root, c_p, c_y, cy, log_n, lp, lsp)) return;
   }
   if (st.flags & VBN_F_LOGP) {
     const float x0 = NODE_X(0);
