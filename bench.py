@@ -141,17 +141,20 @@ def kde_exps_per_particle(model, plan, executed: bool = False) -> float:
     2M for a non-root log-prob (LSE over K_p and over K_p K_y), M for a root log-prob.
     ``executed``: without the CDF pass of nodes whose pass 1 comes from a moment table
     (plan.kde_moment_table: no exps; a wave with a particle off the table's grid falls back to
-    the exp pass, which on-manifold workloads do not do)."""
+    the exp pass, which on-manifold workloads do not do), and with M instead of 2M for the
+    log-prob of a node that is also sampled (its denominator is the sampling pass's total,
+    csrc kde_index_mfma lsp)."""
     exps = 0.0
     for i in range(plan.n_steps):
         row = plan.steps[i].tolist()
         if row[0] != KIND_ID["kde"] or row[1] == 0:
             continue
         m, root = row[9], bool(row[2] & 2)
-        if row[1] == 1 and not root and not (executed and row[31] >= 0):
+        sampled = row[1] == 1 and not root
+        if sampled and not (executed and row[31] >= 0):
             exps += m
         if row[2] & 1:
-            exps += m if root else 2 * m
+            exps += m if (root or (executed and sampled)) else 2 * m
     return exps
 
 
