@@ -1528,6 +1528,7 @@ __device__ __forceinline__ void kde_b32_sums(const bf16x8* __restrict__ pa, int 
 #ifndef KDE_NSUB
 #define KDE_NSUB 2
 #endif
+#define KDE_HALF_MIN 16      // 32-point blocks per chunk below which a chunk is scanned whole
 __device__ __forceinline__ int kde_sub_blocks(int cb32, int k) {
   return ((cb32 * k) / KDE_NSUB) & ~(KDE_PF - 1);
 }
@@ -1769,7 +1770,10 @@ __device__ __forceinline__ int kde_index_mfma(const vbn_walk_args& A, const vbn_
     const bool fform = __all(-negsq <= KDE_FFORM_MAX);
     shift = fform ? 0.f : -negsq;
 #ifndef VBN_ABL_NOHALVES
-    float* hsp = (st.flags & VBN_F_PRE_OUT) ? nullptr : hs;
+    // chunks of >= KDE_HALF_MIN 32-point blocks only: shorter chunks scan little, and the
+    // sums' 64 B of scratch per particle then cost fabric traffic for no time (cfg5, M = 4096:
+    // 8 blocks per chunk, 58.9 ms either way, 27 vs 7 GB per launch)
+    float* hsp = ((st.flags & VBN_F_PRE_OUT) || (cb >> 1) < KDE_HALF_MIN) ? nullptr : hs;
     halves = hsp != nullptr;
 #else
     float* hsp = nullptr;
